@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""Benchmark: numbers checked/sec per node, detailed + niceonly, 1e9 @ base 40
+(BASELINE.json metric; benchmark.rs:60 ExtraLarge field).
+
+One step = one pass of the hot path over one field in BOTH modes: a detailed
+pass (histogram + near-misses) and a niceonly pass (host MSD filter + GPU
+stride candidates), exactly what the reference client does per field
+(client/src/main.rs:120-208, process_range_*_gpu).  Inputs are the field
+bounds only (no host buffers): the kernels derive every n themselves.
+
+Multi-GPU (one process per GPU, torchrun): weak scaling -- rank r processes
+its own consecutive 1e9 field [start + r*1e9, start + (r+1)*1e9) of base 40,
+as independent volunteer claims would; there is no data-path collective.
+Timing: barrier + device sync on both sides of exactly K steps, max over ranks.
+
+    python bench.py [--gpus N --steps K --warmup W] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FIELD_SIZE = 10 ** 9
+BASE = 40
+W_ALG = 4 * BASE                    # int32 VALU ops per n
+PEAK_INT32_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 78.64 Tops/s per MI355X (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0,
+                   help="target CPU work for the bounded cpu_baseline sample")
+    p.add_argument("--mode", choices=["both", "detailed", "niceonly"], default="both")
+    p.add_argument("--msd-floor", type=int, default=0, help="0 = reference CPU-path floor 250")
+    return p.parse_args()
+
+
+def cpu_threads():
+    for k in ("OMP_NUM_THREADS", "MAX_JOBS"):
+        if os.environ.get(k, "").isdigit():
+            return max(1, int(os.environ[k]))
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def cpu_baseline(start, target_s):
+    """Reference algorithm (oracle/ C restatement, 'port') on the host cores,
+    on a bounded sample of the same workload, extrapolated per number."""
+    from oracle import oracle as O
+    th = cpu_threads()
+    # detailed: size the sample to ~target_s of work
+    probe = 4_000_000
+    t = time.perf_counter()
+    O.process_field_detailed_mt(start, start + probe, BASE, th)
+    rate = probe / (time.perf_counter() - t)
+    n = int(min(FIELD_SIZE, max(probe, rate * target_s)))
+    n = max(1_000_000, n // 1_000_000 * 1_000_000)
+    t = time.perf_counter()
+    O.process_field_detailed_mt(start, start + n, BASE, th)
+    td = time.perf_counter() - t
+    det_rate = n / td
+    # niceonly: the whole field (the MSD filter skips most of it at this start)
+    t = time.perf_counter()
+    O.process_field_niceonly_mt(start, start + FIELD_SIZE, BASE, th)
+    tn = time.perf_counter() - t
+    nice_rate = FIELD_SIZE / tn
+    combined = 2 * FIELD_SIZE / (FIELD_SIZE / det_rate + tn)
+    return {"value": combined, "unit": "numbers/s", "cores": th, "kind": "port",
+            "sample": f"detailed: first {n:.3g} n of the field on {th} threads "
+                      f"({det_rate:.3e} n/s, extrapolated to 1e9); niceonly: whole 1e9 field "
+                      f"({nice_rate:.3e} n/s); reference client chunking, MSD floor 250, k=2",
+            "detailed_numbers_per_sec": det_rate, "niceonly_numbers_per_sec": nice_rate}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import nice_amd as N
+
+    ctx = N.GpuContext([local])
+    br = N.get_base_range_u128(BASE)
+    start = br.range_start + rank * FIELD_SIZE
+    end = start + FIELD_SIZE
+    assert end <= br.range_end
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    det_ms, nice_ms, kern_ms = [], [], []
+    last_nice_stats = None
+
+    def step():
+        nonlocal last_nice_stats
+        if args.mode in ("both", "detailed"):
+            t = time.perf_counter()
+            hist, lst = ctx.detailed_raw(start, end, BASE)
+            det_ms.append((time.perf_counter() - t) * 1e3)
+            kern_ms.append(ctx.kernel_stats().kernel_ms)
+            assert sum(hist) == FIELD_SIZE
+        if args.mode in ("both", "niceonly"):
+            t = time.perf_counter()
+            _, st = ctx.niceonly_raw(start, end, BASE, msd_floor=args.msd_floor)
+            nice_ms.append((time.perf_counter() - t) * 1e3)
+            last_nice_stats = st
+
+    for _ in range(args.warmup):
+        step()
+    det_ms.clear(), nice_ms.clear(), kern_ms.clear()
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    modes = 2 if args.mode == "both" else 1
+    total_numbers = modes * FIELD_SIZE * world * args.steps
+    value = total_numbers / elapsed
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    line = {
+        "metric": "numbers checked/sec per node, detailed+niceonly, 1e9 @ base 40 field",
+        "value": value,
+        "unit": "numbers/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (the reference's deterministic benchmark field; n derived on device)",
+        "config": {
+            "workload": "extra-large: 1e9 @ base 40, detailed + niceonly per step "
+                        "(benchmark.rs:60; rank r takes the r-th consecutive 1e9 field)",
+            "base": BASE, "field_start": start - rank * FIELD_SIZE, "field_size": FIELD_SIZE,
+            "mode": args.mode,
+            "niceonly_msd_floor": args.msd_floor or 250,
+            "niceonly_chunking": "reference client (1e6 * clamp(ceil(size/1e11),1,1000))",
+            "parallelism": f"weak{world}",
+        },
+    }
+    if det_ms:
+        kms = sum(kern_ms) / len(kern_ms)
+        achieved = W_ALG * FIELD_SIZE / (kms / 1e3) / 1e12
+        line["detailed_numbers_per_sec"] = FIELD_SIZE / (sum(det_ms) / len(det_ms) / 1e3)
+        line["detailed_ms"] = sum(det_ms) / len(det_ms)
+        line["roofline"] = {
+            "bound": "valu", "kernel": "detailed_fd_kernel<40>",
+            "achieved": achieved, "peak": PEAK_INT32_TOPS, "unit": "int32 Tops/s",
+            "frac": achieved / PEAK_INT32_TOPS, "traffic": None,
+            "kernel_ms": kms,
+            "work_per_unit": f"{W_ALG} int32 ops per n (4 per digit x {BASE} digits, SURVEY 8d)",
+            "note": "integer-VALU bound (no HBM stream, no contraction); kernel time from HIP "
+                    "events on the launch stream; traffic: no input stream (outputs < 1 KB)",
+        }
+    if nice_ms:
+        line["niceonly_numbers_per_sec"] = FIELD_SIZE / (sum(nice_ms) / len(nice_ms) / 1e3)
+        line["niceonly_ms"] = sum(nice_ms) / len(nice_ms)
+        st = last_nice_stats
+        line["niceonly"] = {"ranges": st.ranges, "range_numbers": st.range_numbers,
+                            "candidates": st.candidates, "launches": st.launches,
+                            "msd_seconds": st.msd_seconds, "total_seconds": st.total_seconds}
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(br.range_start, args.cpu_seconds)
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

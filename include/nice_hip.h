@@ -1,0 +1,149 @@
+/*
+ * nice_hip.h -- C ABI of libnice_hip.so, the MI355X (gfx950) field-processing
+ * path of wasabipesto/nice.
+ *
+ * This is the drop-in boundary: plain pointers, sizes and u64 pairs, no torch
+ * or HIP types, so a cgo / Rust FFI / ctypes binding can call it directly
+ * (INTEGRATION.md shows the Rust `extern "C"` shim the reference would add).
+ * Every entry point cites the reference interface it replaces
+ * (paths relative to the reference repository root).
+ *
+ * Conventions
+ *  - u128 values are passed as (lo, hi) u64 pairs, the split the reference
+ *    GPU path already uses (common/src/client_process_gpu.rs:492-499).
+ *  - Ranges are half-open [start, end) like FieldSize (common/src/lib.rs:84-153).
+ *  - Every call returns NICE_OK (0) or an error code; nice_last_error() gives
+ *    a thread-local message (the reference returns anyhow::Result,
+ *    client_process_gpu.rs:777-782, 860-862).
+ *  - Output lists are caller-allocated with a capacity; *n_out always receives
+ *    the true length.  If it exceeds the capacity the call returns
+ *    NICE_ERR_CAPACITY (never a silent truncation) and the caller may retry
+ *    with a larger buffer.
+ */
+#ifndef NICE_HIP_H
+#define NICE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NICE_OK 0
+#define NICE_ERR_INVALID 1     /* bad argument (empty range, base out of 2..128, ...) */
+#define NICE_ERR_HIP 2         /* HIP runtime / kernel failure */
+#define NICE_ERR_CAPACITY 3    /* caller's output list too small; *n_out = needed */
+#define NICE_ERR_NO_DEVICE 4   /* no usable GPU */
+
+/* NiceNumberSimple (common/src/lib.rs:182-186). */
+typedef struct {
+    uint64_t number_lo;
+    uint64_t number_hi;
+    uint32_t num_uniques;
+    uint32_t reserved;
+} nice_number;
+
+typedef struct nice_ctx nice_ctx;
+
+/* GpuContext::new(device_ordinal) (client_process_gpu.rs:215-244), extended to a
+ * list of devices: a field is sharded into contiguous n-ranges, one per device.
+ * No JIT happens here or later: kernels are AOT-built for gfx950. */
+int nice_ctx_create(const int *devices, int n_devices, nice_ctx **out);
+void nice_ctx_destroy(nice_ctx *ctx);
+int nice_device_count(int *out);
+const char *nice_last_error(void);
+
+/* process_range_detailed_gpu(&GpuContext, &FieldSize, base) -> FieldResults
+ * (client_process_gpu.rs:812-897; CPU semantics client_process.rs:150-191).
+ * hist receives base+1 u64 counts indexed by num_uniques (bin 0 is always 0;
+ * FieldResults.distribution is bins 1..=base).  out receives the near-misses
+ * (num_uniques > floor(base * 0.9f)) in ascending order of number. */
+int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi,
+                                uint64_t end_lo, uint64_t end_hi, uint32_t base,
+                                uint64_t *hist, nice_number *out, size_t cap, size_t *n_out);
+
+/* Niceonly tuning (all zero = reference CPU-path semantics, which make the
+ * candidate set identical to process_range_niceonly's):
+ *   msd_floor  MSD recursion floor; 0 -> 250 (msd_prefix_filter.rs:282)
+ *   chunk_size MSD chunking of the field; 0 -> reference client rule
+ *              1e6 * clamp(ceil(size / 1e11), 1, 1000) (client/src/main.rs:158-168)
+ *   threads    host MSD worker threads; 0 -> hardware concurrency
+ *   stride_k   LSD digits in the stride table; 0 -> 2 (client/src/main.rs:19)  */
+typedef struct {
+    uint64_t msd_floor;
+    uint64_t chunk_size;
+    int32_t threads;
+    uint32_t stride_k;
+} nice_niceonly_opts;
+
+typedef struct {
+    uint64_t ranges;        /* MSD-surviving sub-ranges */
+    uint64_t range_numbers; /* numbers inside them */
+    uint64_t candidates;    /* stride candidates checked on the GPU */
+    uint32_t launches;
+    uint32_t reserved;
+    double msd_seconds;     /* until the last MSD worker finished */
+    double total_seconds;
+} nice_niceonly_stats;
+
+/* process_range_niceonly_gpu(&GpuContext, &FieldSize, base) -> FieldResults
+ * (client_process_gpu.rs:515-557; CPU semantics client_process.rs:439-465).
+ * Nice numbers (num_uniques = base) ascending.  Residue-empty bases return an
+ * empty list (client_process_gpu.rs:525-531). */
+int nice_process_range_niceonly(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi,
+                                uint64_t end_lo, uint64_t end_hi, uint32_t base,
+                                nice_number *out, size_t cap, size_t *n_out);
+int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi,
+                                   uint64_t end_lo, uint64_t end_hi, uint32_t base,
+                                   const nice_niceonly_opts *opts, nice_number *out,
+                                   size_t cap, size_t *n_out, nice_niceonly_stats *stats);
+
+/* Device time of the hot kernel(s) in the last detailed call on a device,
+ * measured with HIP events on the launch stream. */
+typedef struct {
+    double kernel_ms;    /* summed over launches */
+    uint32_t launches;
+    uint32_t fd_kernel;  /* 1 if the finite-difference kernel ran */
+    uint64_t numbers;    /* numbers processed by those launches */
+} nice_kernel_stats;
+int nice_last_kernel_stats(nice_ctx *ctx, int device_index, nice_kernel_stats *out);
+
+/* Host helpers mirroring the reference functions the client calls. */
+/* get_base_range_u128 (base_range.rs:43-54): 1 range, 0 none, -1 exceeds u128. */
+int nice_base_range(uint32_t base, uint64_t *start_lo, uint64_t *start_hi, uint64_t *end_lo,
+                    uint64_t *end_hi);
+/* get_near_miss_cutoff (number_stats.rs:15-17). */
+uint32_t nice_near_miss_cutoff(uint32_t base);
+/* pub const GPU_BATCH_SIZE / PROCESSING_CHUNK_SIZE (client_process_gpu.rs:54, 59). */
+uint64_t nice_gpu_batch_size(void);
+uint64_t nice_processing_chunk_size(void);
+/* gpu_supports_base (client_process_gpu.rs:473-476): every base 2..128 runs on
+ * the GPU here (no CPU fallback). */
+int nice_gpu_supports_base(uint32_t base);
+/* 1 if detailed fields of this base inside its range use the FD kernel. */
+int nice_fd_kernel_base(uint32_t base);
+
+/* Host MSD filter, get_valid_ranges_recursive (msd_prefix_filter.rs:583-674)
+ * with max depth 22 and factor 2: writes (start_lo, start_hi, end_lo, end_hi)
+ * quadruples, returns the true count via *n_out. */
+int nice_msd_valid_ranges(uint64_t start_lo, uint64_t start_hi, uint64_t end_lo,
+                          uint64_t end_hi, uint32_t base, uint64_t floor_size, uint64_t *out,
+                          size_t cap, size_t *n_out);
+/* has_duplicate_msd_prefix (msd_prefix_filter.rs:382-563): 1 skippable, 0 not. */
+int nice_msd_skippable(uint64_t start_lo, uint64_t start_hi, uint64_t end_lo, uint64_t end_hi,
+                       uint32_t base);
+/* StrideTable::new(base, k) (stride_filter.rs:40-87): modulus and residue count. */
+int nice_stride_table(uint32_t base, uint32_t k, uint64_t *modulus, uint32_t *residues,
+                      size_t cap, size_t *n_out);
+
+/* Diagnostics: per-n results of the device functions the kernels use. */
+int nice_debug_unique_counts(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t count,
+                             uint32_t base, uint32_t *out);
+int nice_debug_is_nice(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t count, uint32_t base,
+                       uint32_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,260 @@
+"""Host-side mirror of the reference's field-processing API over the C ABI.
+
+Names, argument meaning and error behaviour follow
+common/src/client_process_gpu.rs (GpuContext, process_range_detailed_gpu,
+process_range_niceonly_gpu, process_detailed_gpu, process_niceonly_gpu) and
+common/src/client_process.rs (process_range_detailed, process_range_niceonly,
+which here run on the GPU through a default context -- the drop-in the
+north star asks for).  All compute happens in libnice_hip.so.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+from . import _lib
+from ._lib import check, lib
+from .types import (DataToClient, DataToServer, FieldResults, FieldSize, NiceNumberSimple,
+                    UniquesDistributionSimple)
+
+CLIENT_VERSION = "3.2.15-mi355x"
+MASK64 = (1 << 64) - 1
+
+
+def _split(n: int):
+    if n < 0 or n >> 128:
+        raise ValueError("value must fit in u128")
+    return n & MASK64, n >> 64
+
+
+# pub const GPU_BATCH_SIZE / PROCESSING_CHUNK_SIZE (client_process_gpu.rs:54, 59)
+def _const(name):
+    try:
+        return int(getattr(lib(), name)())
+    except _lib.NiceLibraryError:
+        return None
+
+
+GPU_BATCH_SIZE = 50_000_000
+PROCESSING_CHUNK_SIZE = 1_000_000
+
+
+def get_base_range_u128(base: int) -> Optional[FieldSize]:
+    """get_base_range_u128 (common/src/base_range.rs:43-54)."""
+    a, b, c, d = (ctypes.c_uint64() for _ in range(4))
+    rc = lib().nice_base_range(base, a, b, c, d)
+    if rc < 0:
+        raise OverflowError(f"base {base}: range does not fit in u128")
+    if rc == 0:
+        return None
+    return FieldSize(a.value | (b.value << 64), c.value | (d.value << 64))
+
+
+def get_near_miss_cutoff(base: int) -> int:
+    """get_near_miss_cutoff (common/src/number_stats.rs:15-17)."""
+    return int(lib().nice_near_miss_cutoff(base))
+
+
+def gpu_supports_base(base: int) -> bool:
+    return bool(lib().nice_gpu_supports_base(base))
+
+
+@dataclass
+class StrideTable:
+    """StrideTable (common/src/stride_filter.rs:20-87), host-built by the library."""
+    base: int
+    k: int
+    modulus: int
+    valid_residues: List[int]
+
+    @classmethod
+    def new(cls, base: int, k: int) -> "StrideTable":
+        m = ctypes.c_uint64()
+        n = ctypes.c_size_t()
+        check(lib().nice_stride_table(base, k, m, None, 0, n))
+        buf = (ctypes.c_uint32 * max(n.value, 1))()
+        check(lib().nice_stride_table(base, k, m, buf, n.value, n))
+        return cls(base, k, m.value, list(buf[: n.value]))
+
+
+def get_valid_ranges(range_: FieldSize, base: int, floor_size: int = 250) -> List[FieldSize]:
+    """get_valid_ranges_recursive (common/src/msd_prefix_filter.rs:583-674)."""
+    s, e = range_.range_start, range_.range_end
+    n = ctypes.c_size_t()
+    rc = lib().nice_msd_valid_ranges(*_split(s), *_split(e), base, floor_size, None, 0, n)
+    if rc not in (_lib.NICE_OK, _lib.NICE_ERR_CAPACITY):
+        check(rc)
+    buf = (ctypes.c_uint64 * (4 * max(n.value, 1)))()
+    check(lib().nice_msd_valid_ranges(*_split(s), *_split(e), base, floor_size, buf, n.value, n))
+    return [FieldSize(buf[4 * i] | (buf[4 * i + 1] << 64), buf[4 * i + 2] | (buf[4 * i + 3] << 64))
+            for i in range(n.value)]
+
+
+def has_duplicate_msd_prefix(range_: FieldSize, base: int) -> bool:
+    """has_duplicate_msd_prefix (common/src/msd_prefix_filter.rs:382-563)."""
+    rc = lib().nice_msd_skippable(*_split(range_.range_start), *_split(range_.range_end), base)
+    if rc < 0 or rc > 1:
+        check(rc)
+    return bool(rc)
+
+
+@dataclass
+class NiceonlyStats:
+    ranges: int
+    range_numbers: int
+    candidates: int
+    launches: int
+    msd_seconds: float
+    total_seconds: float
+
+
+@dataclass
+class KernelStats:
+    kernel_ms: float
+    launches: int
+    fd_kernel: bool
+    numbers: int
+
+
+class GpuContext:
+    """GpuContext (client_process_gpu.rs:196-306).  `devices` extends the
+    reference's single ordinal: a field is sharded across the listed GPUs."""
+
+    def __init__(self, devices: Sequence[int] | int = 0):
+        if isinstance(devices, int):
+            devices = [devices]
+        arr = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        check(lib().nice_ctx_create(arr, len(devices), ctypes.byref(h)))
+        self._h = h
+        self.devices = list(devices)
+
+    @classmethod
+    def new(cls, device_ordinal: int = 0) -> "GpuContext":
+        return cls([device_ordinal])
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().nice_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def kernel_stats(self, device_index: int = 0) -> KernelStats:
+        s = _lib.nice_kernel_stats()
+        check(lib().nice_last_kernel_stats(self._h, device_index, s))
+        return KernelStats(s.kernel_ms, s.launches, bool(s.fd_kernel), s.numbers)
+
+    # -- detailed -------------------------------------------------------------
+    def detailed_raw(self, start: int, end: int, base: int, cap: int = 1 << 16):
+        """Histogram (base+1 bins) and near-miss list [(n, u)] ascending."""
+        hist = (ctypes.c_uint64 * (base + 1))()
+        while True:
+            out = (_lib.nice_number * max(cap, 1))()
+            n = ctypes.c_size_t()
+            rc = lib().nice_process_range_detailed(self._h, *_split(start), *_split(end), base,
+                                                   hist, out, cap, n)
+            if rc == _lib.NICE_ERR_CAPACITY:
+                cap = n.value
+                continue
+            check(rc)
+            lst = [(out[i].number_lo | (out[i].number_hi << 64), out[i].num_uniques)
+                   for i in range(n.value)]
+            return list(hist), lst
+
+    # -- niceonly -------------------------------------------------------------
+    def niceonly_raw(self, start: int, end: int, base: int, msd_floor: int = 0,
+                     chunk_size: int = 0, threads: int = 0, stride_k: int = 0,
+                     cap: int = 1 << 16):
+        opts = _lib.nice_niceonly_opts(msd_floor, chunk_size, threads, stride_k)
+        st = _lib.nice_niceonly_stats()
+        while True:
+            out = (_lib.nice_number * max(cap, 1))()
+            n = ctypes.c_size_t()
+            rc = lib().nice_process_range_niceonly_ex(self._h, *_split(start), *_split(end), base,
+                                                      opts, out, cap, n, st)
+            if rc == _lib.NICE_ERR_CAPACITY:
+                cap = n.value
+                continue
+            check(rc)
+            lst = [out[i].number_lo | (out[i].number_hi << 64) for i in range(n.value)]
+            stats = NiceonlyStats(st.ranges, st.range_numbers, st.candidates, st.launches,
+                                  st.msd_seconds, st.total_seconds)
+            return lst, stats
+
+    def debug_unique_counts(self, ns: Sequence[int], base: int) -> List[int]:
+        arr = (ctypes.c_uint64 * (2 * max(len(ns), 1)))()
+        for i, n in enumerate(ns):
+            arr[2 * i], arr[2 * i + 1] = _split(n)
+        out = (ctypes.c_uint32 * max(len(ns), 1))()
+        check(lib().nice_debug_unique_counts(self._h, arr, len(ns), base, out))
+        return list(out[: len(ns)])
+
+    def debug_is_nice(self, ns: Sequence[int], base: int) -> List[bool]:
+        arr = (ctypes.c_uint64 * (2 * max(len(ns), 1)))()
+        for i, n in enumerate(ns):
+            arr[2 * i], arr[2 * i + 1] = _split(n)
+        out = (ctypes.c_uint32 * max(len(ns), 1))()
+        check(lib().nice_debug_is_nice(self._h, arr, len(ns), base, out))
+        return [bool(x) for x in out[: len(ns)]]
+
+
+def process_range_detailed_gpu(ctx: GpuContext, range_: FieldSize, base: int) -> FieldResults:
+    """process_range_detailed_gpu (client_process_gpu.rs:812-897)."""
+    hist, lst = ctx.detailed_raw(range_.range_start, range_.range_end, base)
+    return FieldResults(
+        distribution=[UniquesDistributionSimple(i, hist[i]) for i in range(1, base + 1)],
+        nice_numbers=[NiceNumberSimple(n, u) for n, u in lst])
+
+
+def process_range_niceonly_gpu(ctx: GpuContext, range_: FieldSize, base: int,
+                               **opts) -> FieldResults:
+    """process_range_niceonly_gpu (client_process_gpu.rs:515-557)."""
+    lst, _ = ctx.niceonly_raw(range_.range_start, range_.range_end, base, **opts)
+    return FieldResults(distribution=[], nice_numbers=[NiceNumberSimple(n, base) for n in lst])
+
+
+def process_detailed_gpu(ctx: GpuContext, claim: DataToClient, username: str) -> DataToServer:
+    """process_detailed_gpu (client_process_gpu.rs:907-922)."""
+    r = process_range_detailed_gpu(ctx, claim.field(), claim.base)
+    return DataToServer(claim.claim_id, username, CLIENT_VERSION, r.distribution, r.nice_numbers)
+
+
+def process_niceonly_gpu(ctx: GpuContext, claim: DataToClient, username: str) -> DataToServer:
+    """process_niceonly_gpu (client_process_gpu.rs:924-941)."""
+    r = process_range_niceonly_gpu(ctx, claim.field(), claim.base)
+    return DataToServer(claim.claim_id, username, CLIENT_VERSION, None, r.nice_numbers)
+
+
+_default_ctx: Optional[GpuContext] = None
+_default_lock = threading.Lock()
+
+
+def default_context() -> GpuContext:
+    global _default_ctx
+    with _default_lock:
+        if _default_ctx is None:
+            _default_ctx = GpuContext(0)
+        return _default_ctx
+
+
+def process_range_detailed(range_: FieldSize, base: int) -> FieldResults:
+    """Drop-in for process_range_detailed (client_process.rs:150-191), on the GPU."""
+    return process_range_detailed_gpu(default_context(), range_, base)
+
+
+def process_range_niceonly(range_: FieldSize, base: int,
+                           stride_table: Optional[StrideTable] = None) -> FieldResults:
+    """Drop-in for process_range_niceonly (client_process.rs:439-465), on the GPU,
+    with the CPU path's candidate set (MSD floor 250 over the whole range, stride
+    table k from `stride_table`, default 2)."""
+    k = stride_table.k if stride_table is not None else 2
+    size = range_.range_size
+    return process_range_niceonly_gpu(default_context(), range_, base, stride_k=k,
+                                      chunk_size=min(size, (1 << 64) - 1))

@@ -1,0 +1,653 @@
+// nice_abi.cpp -- C ABI (include/nice_hip.h) over the gfx950 kernels.
+//
+// Replaces the reference's CUDA host pipeline (common/src/client_process_gpu.rs):
+// no NVRTC (kernels are AOT code objects), one HIP stream per device, fields
+// sharded across devices as contiguous n-ranges, histograms summed and
+// near-miss / nice lists merged on the host, and a multi-threaded host MSD
+// producer streaming range descriptors to the niceonly kernel.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/nice_hip.h"
+#include "host_math.hpp"
+#include "kernels.h"
+
+using nice::u128;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                    \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(NICE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+inline u128 mk(uint64_t lo, uint64_t hi) { return ((u128)hi << 64) | lo; }
+inline uint64_t lo64(u128 v) { return (uint64_t)v; }
+inline uint64_t hi64(u128 v) { return (uint64_t)(v >> 64); }
+
+constexpr uint32_t kInitialListCap = 1u << 20;  // NEAR_MISS_CAPACITY (client_process_gpu.rs:74)
+constexpr uint32_t kNiceCap = 1u << 16;         // NICE_OUT_CAPACITY (:71)
+constexpr uint32_t kBatchRanges = 1u << 16;     // LAUNCH_BATCH_RANGES (:583)
+
+struct DescBuf {
+    // host pinned staging + device copies for one niceonly launch
+    uint64_t *h_b0 = nullptr, *d_b0 = nullptr;
+    uint32_t *h_g0 = nullptr, *d_g0 = nullptr;
+    uint64_t *h_prefix = nullptr, *d_prefix = nullptr;
+    uint32_t cap = 0;
+    hipEvent_t done = nullptr;
+    bool pending = false;
+};
+
+struct Device {
+    int id = 0;
+    int num_cus = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_done = nullptr;
+    uint64_t *d_hist = nullptr;   // 129 bins
+    uint32_t *d_count = nullptr;  // list counters [0] detailed, [1] niceonly
+    uint64_t *d_list_n = nullptr;
+    uint32_t *d_list_u = nullptr;
+    uint32_t list_cap = 0;
+    uint64_t *h_hist = nullptr;   // pinned
+    uint32_t *h_count = nullptr;  // pinned
+    std::map<uint32_t, uint32_t *> residues;  // base -> device residue table
+    DescBuf desc[2];
+    int desc_next = 0;
+    nice_kernel_stats last{};
+};
+
+struct StrideCache {
+    std::mutex mu;
+    std::map<std::pair<uint32_t, uint32_t>, std::shared_ptr<nice::StrideTable>> tables;
+    std::shared_ptr<nice::StrideTable> get(uint32_t base, uint32_t k) {
+        std::lock_guard<std::mutex> g(mu);
+        auto key = std::make_pair(base, k);
+        auto it = tables.find(key);
+        if (it != tables.end()) return it->second;
+        auto t = std::make_shared<nice::StrideTable>(base, k);
+        tables[key] = t;
+        return t;
+    }
+};
+StrideCache g_stride;
+
+}  // namespace
+
+struct nice_ctx {
+    std::vector<Device> devs;
+    std::mutex mu;  // one in-flight field per context (client_process_gpu.rs:196-201)
+};
+
+namespace {
+
+int ensure_list(Device &d, uint32_t cap) {
+    if (d.list_cap >= cap) return NICE_OK;
+    HIPCHK(hipSetDevice(d.id));
+    if (d.d_list_n) HIPCHK(hipFree(d.d_list_n));
+    if (d.d_list_u) HIPCHK(hipFree(d.d_list_u));
+    HIPCHK(hipMalloc(&d.d_list_n, (size_t)cap * 16));
+    HIPCHK(hipMalloc(&d.d_list_u, (size_t)cap * 4));
+    d.list_cap = cap;
+    return NICE_OK;
+}
+
+int ensure_desc(DescBuf &b, uint32_t cap) {
+    if (b.cap >= cap) return NICE_OK;
+    if (b.pending) HIPCHK(hipEventSynchronize(b.done));
+    b.pending = false;
+    if (b.h_b0) {
+        HIPCHK(hipHostFree(b.h_b0));
+        HIPCHK(hipHostFree(b.h_g0));
+        HIPCHK(hipHostFree(b.h_prefix));
+        HIPCHK(hipFree(b.d_b0));
+        HIPCHK(hipFree(b.d_g0));
+        HIPCHK(hipFree(b.d_prefix));
+    }
+    HIPCHK(hipHostMalloc(&b.h_b0, (size_t)cap * 16, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(&b.h_g0, (size_t)cap * 4, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(&b.h_prefix, (size_t)(cap + 1) * 8, hipHostMallocDefault));
+    HIPCHK(hipMalloc(&b.d_b0, (size_t)cap * 16));
+    HIPCHK(hipMalloc(&b.d_g0, (size_t)cap * 4));
+    HIPCHK(hipMalloc(&b.d_prefix, (size_t)(cap + 1) * 8));
+    if (!b.done) HIPCHK(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
+    b.cap = cap;
+    return NICE_OK;
+}
+
+int device_init(Device &d, int id) {
+    d.id = id;
+    HIPCHK(hipSetDevice(id));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, id));
+    d.num_cus = prop.multiProcessorCount;
+    HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&d.ev0));
+    HIPCHK(hipEventCreate(&d.ev1));
+    HIPCHK(hipEventCreateWithFlags(&d.ev_done, hipEventDisableTiming));
+    HIPCHK(hipMalloc(&d.d_hist, 129 * 8));
+    HIPCHK(hipMalloc(&d.d_count, 2 * 4));
+    HIPCHK(hipHostMalloc(&d.h_hist, 129 * 8, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(&d.h_count, 2 * 4, hipHostMallocDefault));
+    int rc = ensure_list(d, kInitialListCap);
+    if (rc) return rc;
+    return NICE_OK;
+}
+
+void device_free(Device &d) {
+    if (!d.stream) return;
+    (void)hipSetDevice(d.id);
+    (void)hipStreamSynchronize(d.stream);
+    for (auto &kv : d.residues) (void)hipFree(kv.second);
+    for (auto &b : d.desc) {
+        if (b.h_b0) {
+            (void)hipHostFree(b.h_b0);
+            (void)hipHostFree(b.h_g0);
+            (void)hipHostFree(b.h_prefix);
+            (void)hipFree(b.d_b0);
+            (void)hipFree(b.d_g0);
+            (void)hipFree(b.d_prefix);
+        }
+        if (b.done) (void)hipEventDestroy(b.done);
+    }
+    (void)hipFree(d.d_hist);
+    (void)hipFree(d.d_count);
+    (void)hipFree(d.d_list_n);
+    (void)hipFree(d.d_list_u);
+    (void)hipHostFree(d.h_hist);
+    (void)hipHostFree(d.h_count);
+    (void)hipEventDestroy(d.ev0);
+    (void)hipEventDestroy(d.ev1);
+    (void)hipEventDestroy(d.ev_done);
+    (void)hipStreamDestroy(d.stream);
+    d.stream = nullptr;
+}
+
+struct Entry {
+    u128 n;
+    uint32_t u;
+};
+
+int emit_list(std::vector<Entry> &all, nice_number *out, size_t cap, size_t *n_out) {
+    std::sort(all.begin(), all.end(), [](const Entry &a, const Entry &b) { return a.n < b.n; });
+    if (n_out) *n_out = all.size();
+    const size_t c = std::min(cap, all.size());
+    for (size_t i = 0; i < c; i++) {
+        out[i].number_lo = lo64(all[i].n);
+        out[i].number_hi = hi64(all[i].n);
+        out[i].num_uniques = all[i].u;
+        out[i].reserved = 0;
+    }
+    if (all.size() > cap)
+        return fail(NICE_ERR_CAPACITY, "output list needs " + std::to_string(all.size()) +
+                                           " entries, capacity " + std::to_string(cap));
+    return NICE_OK;
+}
+
+// Enqueue the detailed kernels for [s, e) on one device (async).
+int enqueue_detailed(Device &d, u128 s, u128 e, uint32_t base, bool &used_fd, uint64_t &fd_count) {
+    nice::DetailedLaunch p{};
+    p.base = base;
+    p.cutoff = nice::near_miss_cutoff(base);
+    p.hist = d.d_hist;
+    p.out = nice::NumOut{d.d_list_n, d.d_list_u, d.d_count, d.list_cap};
+    auto launch = [&](u128 a, u128 b, bool fd) -> int {
+        if (a >= b) return NICE_OK;
+        u128 cnt = b - a;
+        while (cnt) {  // segments longer than 2^63 are split (count is u64)
+            uint64_t c = cnt > ((u128)1 << 62) ? (1ull << 62) : (uint64_t)cnt;
+            p.start_lo = lo64(a);
+            p.start_hi = hi64(a);
+            p.count = c;
+            hipError_t err = fd ? nice::launch_detailed_fd(p, d.num_cus, d.stream)
+                                : nice::launch_detailed_generic(p, d.num_cus, d.stream);
+            if (err != hipSuccess)
+                return fail(NICE_ERR_HIP, std::string("detailed launch: ") + hipGetErrorString(err));
+            if (fd) {
+                used_fd = true;
+                fd_count += c;
+            }
+            a += c;
+            cnt -= c;
+        }
+        return NICE_OK;
+    };
+    u128 rs = 0, re = 0;
+    const bool fd = nice::fd_supported(base) && nice::base_range(base, rs, re) == 1;
+    if (!fd) return launch(s, e, false);
+    int rc;
+    if ((rc = launch(s, std::min(e, rs), false))) return rc;
+    if ((rc = launch(std::max(s, rs), std::min(e, re), true))) return rc;
+    return launch(std::max(s, re), e, false);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *nice_last_error(void) { return g_err.c_str(); }
+
+int nice_device_count(int *out) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *out = n;
+    return NICE_OK;
+}
+
+int nice_ctx_create(const int *devices, int n_devices, nice_ctx **out) {
+    if (!out) return fail(NICE_ERR_INVALID, "null out");
+    int have = 0;
+    if (hipGetDeviceCount(&have) != hipSuccess || have < 1)
+        return fail(NICE_ERR_NO_DEVICE, "no HIP device visible");
+    std::unique_ptr<nice_ctx> ctx(new nice_ctx());
+    std::vector<int> ids;
+    if (!devices || n_devices <= 0) ids.push_back(0);
+    else ids.assign(devices, devices + n_devices);
+    ctx->devs.resize(ids.size());
+    for (size_t i = 0; i < ids.size(); i++) {
+        if (ids[i] < 0 || ids[i] >= have)
+            return fail(NICE_ERR_INVALID, "device ordinal " + std::to_string(ids[i]) + " out of range");
+        int rc = device_init(ctx->devs[i], ids[i]);
+        if (rc) {
+            for (auto &d : ctx->devs) device_free(d);
+            return rc;
+        }
+    }
+    *out = ctx.release();
+    return NICE_OK;
+}
+
+void nice_ctx_destroy(nice_ctx *ctx) {
+    if (!ctx) return;
+    for (auto &d : ctx->devs) device_free(d);
+    delete ctx;
+}
+
+int nice_base_range(uint32_t base, uint64_t *slo, uint64_t *shi, uint64_t *elo, uint64_t *ehi) {
+    u128 s = 0, e = 0;
+    int rc = nice::base_range(base, s, e);
+    if (rc == 1) {
+        *slo = lo64(s);
+        *shi = hi64(s);
+        *elo = lo64(e);
+        *ehi = hi64(e);
+    }
+    return rc;
+}
+
+uint32_t nice_near_miss_cutoff(uint32_t base) { return nice::near_miss_cutoff(base); }
+uint64_t nice_gpu_batch_size(void) { return 50000000ull; }
+uint64_t nice_processing_chunk_size(void) { return 1000000ull; }
+int nice_gpu_supports_base(uint32_t base) { return base >= 2 && base <= 128; }
+int nice_fd_kernel_base(uint32_t base) { return nice::fd_supported(base) ? 1 : 0; }
+
+int nice_last_kernel_stats(nice_ctx *ctx, int i, nice_kernel_stats *out) {
+    if (!ctx || i < 0 || i >= (int)ctx->devs.size() || !out) return fail(NICE_ERR_INVALID, "bad args");
+    *out = ctx->devs[i].last;
+    return NICE_OK;
+}
+
+int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi,
+                                uint64_t end_lo, uint64_t end_hi, uint32_t base, uint64_t *hist,
+                                nice_number *out, size_t cap, size_t *n_out) {
+    if (!ctx || !hist) return fail(NICE_ERR_INVALID, "null argument");
+    if (base < 2 || base > 128) return fail(NICE_ERR_INVALID, "base must be in 2..=128");
+    const u128 s = mk(start_lo, start_hi), e = mk(end_lo, end_hi);
+    if (s >= e)
+        return fail(NICE_ERR_INVALID, "Range has invalid bounds, range_start must be < range_end");
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    const size_t nd = ctx->devs.size();
+    const u128 size = e - s;
+    // Shard bounds: contiguous, in device order (ascending n).
+    std::vector<u128> bounds(nd + 1);
+    for (size_t i = 0; i <= nd; i++) bounds[i] = s + size / nd * i + std::min<u128>(i, size % nd);
+    for (size_t i = 0; i < nd; i++) {
+        Device &d = ctx->devs[i];
+        d.last = nice_kernel_stats{};
+        if (bounds[i] >= bounds[i + 1]) continue;
+        HIPCHK(hipSetDevice(d.id));
+        HIPCHK(hipMemsetAsync(d.d_hist, 0, 129 * 8, d.stream));
+        HIPCHK(hipMemsetAsync(d.d_count, 0, 8, d.stream));
+        HIPCHK(hipEventRecord(d.ev0, d.stream));
+        bool used_fd = false;
+        uint64_t fdc = 0;
+        int rc = enqueue_detailed(d, bounds[i], bounds[i + 1], base, used_fd, fdc);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(d.ev1, d.stream));
+        HIPCHK(hipMemcpyAsync(d.h_hist, d.d_hist, (base + 1) * 8, hipMemcpyDeviceToHost, d.stream));
+        HIPCHK(hipMemcpyAsync(d.h_count, d.d_count, 4, hipMemcpyDeviceToHost, d.stream));
+        HIPCHK(hipEventRecord(d.ev_done, d.stream));
+        d.last.fd_kernel = used_fd;
+        d.last.numbers = (uint64_t)(bounds[i + 1] - bounds[i]);
+        d.last.launches = 1;
+    }
+    std::vector<uint64_t> total(base + 1, 0);
+    std::vector<Entry> all;
+    for (size_t i = 0; i < nd; i++) {
+        Device &d = ctx->devs[i];
+        if (bounds[i] >= bounds[i + 1]) continue;
+        HIPCHK(hipSetDevice(d.id));
+        HIPCHK(hipEventSynchronize(d.ev_done));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, d.ev0, d.ev1));
+        d.last.kernel_ms = ms;
+        uint32_t cnt = d.h_count[0];
+        if (cnt > d.list_cap) {
+            // Near-miss list overflowed (e.g. out-of-range n, SURVEY hazard 9):
+            // grow to the exact count and redo this shard.
+            int rc = ensure_list(d, cnt);
+            if (rc) return rc;
+            HIPCHK(hipMemsetAsync(d.d_hist, 0, 129 * 8, d.stream));
+            HIPCHK(hipMemsetAsync(d.d_count, 0, 8, d.stream));
+            bool used_fd = false;
+            uint64_t fdc = 0;
+            rc = enqueue_detailed(d, bounds[i], bounds[i + 1], base, used_fd, fdc);
+            if (rc) return rc;
+            HIPCHK(hipMemcpyAsync(d.h_hist, d.d_hist, (base + 1) * 8, hipMemcpyDeviceToHost, d.stream));
+            HIPCHK(hipMemcpyAsync(d.h_count, d.d_count, 4, hipMemcpyDeviceToHost, d.stream));
+            HIPCHK(hipStreamSynchronize(d.stream));
+            cnt = d.h_count[0];
+            if (cnt > d.list_cap) return fail(NICE_ERR_HIP, "near-miss list overflow after resize");
+        }
+        for (uint32_t b = 0; b <= base; b++) total[b] += d.h_hist[b];
+        if (cnt) {
+            std::vector<uint64_t> nbuf((size_t)cnt * 2);
+            std::vector<uint32_t> ubuf(cnt);
+            HIPCHK(hipMemcpy(nbuf.data(), d.d_list_n, (size_t)cnt * 16, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(ubuf.data(), d.d_list_u, (size_t)cnt * 4, hipMemcpyDeviceToHost));
+            for (uint32_t q = 0; q < cnt; q++) all.push_back({mk(nbuf[2 * q], nbuf[2 * q + 1]), ubuf[q]});
+        }
+    }
+    std::memcpy(hist, total.data(), (base + 1) * 8);
+    // Self-check (the server's submit invariants, api/src/main.rs:309-359):
+    // counts sum to the field size and every near-miss bin matches the list.
+    u128 sum = 0;
+    for (uint32_t b = 0; b <= base; b++) sum += total[b];
+    if (sum != size) return fail(NICE_ERR_HIP, "histogram does not sum to the field size");
+    return emit_list(all, out, cap, n_out);
+}
+
+int nice_debug_unique_counts(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t count,
+                             uint32_t base, uint32_t *out) {
+    if (!ctx || base < 2 || base > 128) return fail(NICE_ERR_INVALID, "bad args");
+    if (count == 0) return NICE_OK;
+    Device &d = ctx->devs[0];
+    HIPCHK(hipSetDevice(d.id));
+    uint64_t *dn;
+    uint32_t *du;
+    HIPCHK(hipMalloc(&dn, (size_t)count * 16));
+    HIPCHK(hipMalloc(&du, (size_t)count * 4));
+    HIPCHK(hipMemcpy(dn, n_pairs, (size_t)count * 16, hipMemcpyHostToDevice));
+    HIPCHK(nice::launch_unique_counts(dn, count, base, du, d.stream));
+    HIPCHK(hipStreamSynchronize(d.stream));
+    HIPCHK(hipMemcpy(out, du, (size_t)count * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipFree(dn));
+    HIPCHK(hipFree(du));
+    return NICE_OK;
+}
+
+int nice_debug_is_nice(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t count, uint32_t base,
+                       uint32_t *out) {
+    if (!ctx || base < 2 || base > 128) return fail(NICE_ERR_INVALID, "bad args");
+    if (count == 0) return NICE_OK;
+    Device &d = ctx->devs[0];
+    HIPCHK(hipSetDevice(d.id));
+    uint64_t *dn;
+    uint32_t *du;
+    HIPCHK(hipMalloc(&dn, (size_t)count * 16));
+    HIPCHK(hipMalloc(&du, (size_t)count * 4));
+    HIPCHK(hipMemcpy(dn, n_pairs, (size_t)count * 16, hipMemcpyHostToDevice));
+    HIPCHK(nice::launch_is_nice(dn, count, base, du, d.stream));
+    HIPCHK(hipStreamSynchronize(d.stream));
+    HIPCHK(hipMemcpy(out, du, (size_t)count * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipFree(dn));
+    HIPCHK(hipFree(du));
+    return NICE_OK;
+}
+
+int nice_msd_skippable(uint64_t slo, uint64_t shi, uint64_t elo, uint64_t ehi, uint32_t base) {
+    if (base < 2 || base > 128 || mk(slo, shi) >= mk(elo, ehi)) return fail(NICE_ERR_INVALID, "bad args");
+    return nice::MsdFilter(base).skippable(mk(slo, shi), mk(elo, ehi)) ? 1 : 0;
+}
+
+int nice_msd_valid_ranges(uint64_t slo, uint64_t shi, uint64_t elo, uint64_t ehi, uint32_t base,
+                          uint64_t floor_size, uint64_t *out, size_t cap, size_t *n_out) {
+    if (base < 2 || base > 128 || mk(slo, shi) >= mk(elo, ehi)) return fail(NICE_ERR_INVALID, "bad args");
+    nice::MsdFilter f(base);
+    size_t n = 0;
+    f.valid_ranges(mk(slo, shi), mk(elo, ehi), 0, floor_size, [&](u128 a, u128 b) {
+        if (n < cap) {
+            out[4 * n] = lo64(a);
+            out[4 * n + 1] = hi64(a);
+            out[4 * n + 2] = lo64(b);
+            out[4 * n + 3] = hi64(b);
+        }
+        n++;
+    });
+    *n_out = n;
+    return n > cap ? fail(NICE_ERR_CAPACITY, "range list exceeds capacity") : NICE_OK;
+}
+
+int nice_stride_table(uint32_t base, uint32_t k, uint64_t *modulus, uint32_t *residues,
+                      size_t cap, size_t *n_out) {
+    if (base < 3 || base > 128 || k > 3) return fail(NICE_ERR_INVALID, "bad args");
+    auto t = g_stride.get(base, k);
+    *modulus = t->modulus;
+    *n_out = t->residues.size();
+    for (size_t i = 0; i < std::min(cap, t->residues.size()); i++) residues[i] = t->residues[i];
+    return t->residues.size() > cap && residues ? fail(NICE_ERR_CAPACITY, "capacity") : NICE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Niceonly: multi-threaded host MSD producer -> descriptor batches -> GPU.
+// ---------------------------------------------------------------------------
+int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi,
+                                   uint64_t end_lo, uint64_t end_hi, uint32_t base,
+                                   const nice_niceonly_opts *opts, nice_number *out, size_t cap,
+                                   size_t *n_out, nice_niceonly_stats *stats) {
+    using clock = std::chrono::steady_clock;
+    const auto t0 = clock::now();
+    if (!ctx) return fail(NICE_ERR_INVALID, "null ctx");
+    if (base < 3 || base > 128) return fail(NICE_ERR_INVALID, "base must be in 3..=128");
+    const u128 s = mk(start_lo, start_hi), e = mk(end_lo, end_hi);
+    if (s >= e)
+        return fail(NICE_ERR_INVALID, "Range has invalid bounds, range_start must be < range_end");
+    nice_niceonly_stats st{};
+    const uint64_t floor_size = opts && opts->msd_floor ? opts->msd_floor : 250;
+    const uint32_t k = opts && opts->stride_k ? opts->stride_k : 2;
+    int threads = opts && opts->threads > 0 ? opts->threads : (int)std::thread::hardware_concurrency();
+    if (threads < 1) threads = 1;
+    const u128 chunk = opts && opts->chunk_size ? (u128)opts->chunk_size : nice::client_chunk_size(e - s);
+
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    if (nice::residue_filter(base).empty()) {  // client_process_gpu.rs:525-531
+        if (stats) *stats = st;
+        if (n_out) *n_out = 0;
+        return NICE_OK;
+    }
+    auto table = g_stride.get(base, k);
+    const uint32_t R = (uint32_t)table->residues.size();
+    const uint64_t M = table->modulus;
+    if (M > 0xffffffffull) return fail(NICE_ERR_INVALID, "stride modulus exceeds u32");
+    for (auto &d : ctx->devs) {
+        HIPCHK(hipSetDevice(d.id));
+        if (!d.residues.count(base * 8 + k)) {
+            uint32_t *p;
+            HIPCHK(hipMalloc(&p, (size_t)R * 4));
+            HIPCHK(hipMemcpy(p, table->residues.data(), (size_t)R * 4, hipMemcpyHostToDevice));
+            d.residues[base * 8 + k] = p;
+        }
+        HIPCHK(hipMemsetAsync(d.d_count + 1, 0, 4, d.stream));
+        int rc = ensure_list(d, kNiceCap);
+        if (rc) return rc;
+    }
+
+    // Producer: worker threads run the MSD filter per chunk and hand the
+    // surviving ranges to this thread in chunk batches.
+    const uint64_t nchunks = (uint64_t)((e - s + chunk - 1) / chunk);
+    std::atomic<uint64_t> next{0};
+    std::mutex qmu;
+    std::condition_variable qcv;
+    std::deque<std::vector<std::pair<u128, u128>>> queue;
+    int live = std::min<uint64_t>(threads, nchunks);
+    std::vector<std::thread> workers;
+    nice::MsdFilter filt(base);
+    for (int t = 0; t < live; t++) {
+        workers.emplace_back([&]() {
+            std::vector<std::pair<u128, u128>> local;
+            for (;;) {
+                uint64_t i = next.fetch_add(1);
+                if (i >= nchunks) break;
+                u128 cs = s + (u128)i * chunk;
+                u128 ce = std::min(e, cs + chunk);
+                filt.valid_ranges(cs, ce, 0, floor_size,
+                                  [&](u128 a, u128 b) { local.emplace_back(a, b); });
+                if (local.size() >= 4096) {
+                    std::lock_guard<std::mutex> g(qmu);
+                    queue.push_back(std::move(local));
+                    local = {};
+                    qcv.notify_one();
+                }
+            }
+            std::lock_guard<std::mutex> g(qmu);
+            if (!local.empty()) queue.push_back(std::move(local));
+            live--;
+            qcv.notify_one();
+        });
+    }
+
+    // Consumer: build descriptors and launch on devices round-robin.
+    int rc = NICE_OK;
+    size_t dev_rr = 0;
+    std::vector<std::pair<u128, u128>> pend;
+    auto flush = [&]() -> int {
+        if (pend.empty()) return NICE_OK;
+        Device &d = ctx->devs[dev_rr++ % ctx->devs.size()];
+        HIPCHK(hipSetDevice(d.id));
+        DescBuf &b = d.desc[d.desc_next];
+        d.desc_next ^= 1;
+        // Descriptor count: one per range, more for ranges holding over 2^30
+        // candidates (the kernel's residue-sequence index is 32-bit).
+        constexpr u128 kPiece = (u128)1 << 30;
+        size_t need = 0;
+        for (auto &pr : pend) {
+            const u128 c = table->index_of(pr.second) - table->index_of(pr.first);
+            need += (size_t)((c + kPiece - 1) / kPiece);
+        }
+        int r = ensure_desc(b, (uint32_t)std::max<size_t>(need, 1));
+        if (r) return r;
+        if (b.pending) HIPCHK(hipEventSynchronize(b.done));
+        uint32_t nr = 0;
+        uint64_t total = 0;
+        for (auto &pr : pend) {
+            const u128 i0 = table->index_of(pr.first), i1 = table->index_of(pr.second);
+            st.ranges++;
+            st.range_numbers += (uint64_t)(pr.second - pr.first);
+            for (u128 g = i0; g < i1; g += kPiece) {
+                // candidate g of the global residue sequence: (g / R) * M + res[g % R]
+                const u128 cyc = g / R;
+                const u128 bs = cyc * M;
+                b.h_b0[2 * nr] = lo64(bs);
+                b.h_b0[2 * nr + 1] = hi64(bs);
+                b.h_g0[nr] = (uint32_t)(g - cyc * R);
+                b.h_prefix[nr] = total;
+                total += (uint64_t)std::min<u128>(kPiece, i1 - g);
+                nr++;
+            }
+        }
+        pend.clear();
+        if (!nr) return NICE_OK;
+        b.h_prefix[nr] = total;
+        st.candidates += total;
+        HIPCHK(hipMemcpyAsync(b.d_b0, b.h_b0, (size_t)nr * 16, hipMemcpyHostToDevice, d.stream));
+        HIPCHK(hipMemcpyAsync(b.d_g0, b.h_g0, (size_t)nr * 4, hipMemcpyHostToDevice, d.stream));
+        HIPCHK(hipMemcpyAsync(b.d_prefix, b.h_prefix, (size_t)(nr + 1) * 8, hipMemcpyHostToDevice,
+                              d.stream));
+        nice::NiceonlyLaunch p{};
+        p.b0 = b.d_b0;
+        p.g0 = b.d_g0;
+        p.prefix = b.d_prefix;
+        p.n_ranges = nr;
+        p.total = total;
+        p.residues = d.residues[base * 8 + k];
+        p.R = R;
+        p.M = (uint32_t)M;
+        p.base = base;
+        p.out = nice::NumOut{d.d_list_n, nullptr, d.d_count + 1, d.list_cap};
+        hipError_t err = nice::launch_niceonly(p, d.num_cus, d.stream);
+        if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("niceonly launch: ") + hipGetErrorString(err));
+        HIPCHK(hipEventRecord(b.done, d.stream));
+        b.pending = true;
+        st.launches++;
+        return NICE_OK;
+    };
+    for (;;) {
+        std::vector<std::pair<u128, u128>> item;
+        {
+            std::unique_lock<std::mutex> g(qmu);
+            qcv.wait(g, [&] { return !queue.empty() || live == 0; });
+            if (queue.empty() && live == 0) break;
+            item = std::move(queue.front());
+            queue.pop_front();
+        }
+        if (rc) continue;  // drain the producers after a failure
+        pend.insert(pend.end(), item.begin(), item.end());
+        if (pend.size() >= kBatchRanges) rc = flush();
+    }
+    for (auto &w : workers) w.join();
+    st.msd_seconds = std::chrono::duration<double>(clock::now() - t0).count();
+    if (!rc) rc = flush();
+    if (rc) return rc;
+
+    std::vector<Entry> all;
+    for (auto &d : ctx->devs) {
+        HIPCHK(hipSetDevice(d.id));
+        HIPCHK(hipMemcpyAsync(d.h_count + 1, d.d_count + 1, 4, hipMemcpyDeviceToHost, d.stream));
+        HIPCHK(hipStreamSynchronize(d.stream));
+        for (auto &b : d.desc) b.pending = false;
+        uint32_t cnt = d.h_count[1];
+        if (cnt > d.list_cap)
+            return fail(NICE_ERR_HIP, "niceonly output buffer overflow: " + std::to_string(cnt) +
+                                          " (this strongly suggests a kernel bug)");
+        if (cnt) {
+            std::vector<uint64_t> nbuf((size_t)cnt * 2);
+            HIPCHK(hipMemcpy(nbuf.data(), d.d_list_n, (size_t)cnt * 16, hipMemcpyDeviceToHost));
+            for (uint32_t q = 0; q < cnt; q++) all.push_back({mk(nbuf[2 * q], nbuf[2 * q + 1]), base});
+        }
+    }
+    st.total_seconds = std::chrono::duration<double>(clock::now() - t0).count();
+    if (stats) *stats = st;
+    return emit_list(all, out, cap, n_out);
+}
+
+int nice_process_range_niceonly(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi,
+                                uint64_t end_lo, uint64_t end_hi, uint32_t base, nice_number *out,
+                                size_t cap, size_t *n_out) {
+    return nice_process_range_niceonly_ex(ctx, start_lo, start_hi, end_lo, end_hi, base, nullptr,
+                                          out, cap, n_out, nullptr);
+}
+
+}  // extern "C"

@@ -1,0 +1,233 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the
+committed golden fixtures.  Bit-exact: histograms, near-miss lists, nice lists.
+
+Run on the MI355X box:  python -m pytest tests -m gpu -x -q
+"""
+import json
+import os
+import random
+
+import pytest
+
+import nice_amd as N
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = N.GpuContext(0)
+    yield c
+    c.close()
+
+
+def _dist(hist):
+    return [(i, hist[i]) for i in range(1, len(hist))]
+
+
+def check_detailed(ctx, start, end, base, want=None):
+    hist, lst = ctx.detailed_raw(start, end, base)
+    if want is None:
+        want = O.process_range_detailed(start, end, base, cap=end - start)
+    assert hist[0] == 0
+    assert _dist(hist) == want.distribution, (base, start, end)
+    assert lst == want.nice_numbers, (base, start, end)
+    return hist, lst
+
+
+# --- reference golden vectors (client_process.rs:473-1053) -------------------
+def test_reference_detailed_vectors(ctx, golden):
+    for c in golden["reference"]["detailed"]:
+        b = c["base"]
+        s, e = O.base_range(b)
+        if c["size"]:
+            e = s + c["size"]
+        hist, lst = ctx.detailed_raw(s, e, b)
+        assert _dist(hist) == [tuple(x) for x in c["distribution"]], c["source"]
+        assert lst == [tuple(x) for x in c["nice_numbers"]], c["source"]
+
+
+# --- reference-Python-mirror vectors (tests/golden/python_vectors.json) -------
+def test_python_detailed_vectors(ctx, golden):
+    for c in golden["python"]["detailed"]:
+        hist, lst = ctx.detailed_raw(int(c["start"]), int(c["end"]), c["base"])
+        assert _dist(hist) == [tuple(x) for x in c["distribution"]], c["name"]
+        assert lst == [(int(n), u) for n, u in c["near_misses"]], c["name"]
+
+
+def test_reference_gpu_test_ranges(ctx):
+    # client_process_gpu.rs:1478-1498: (b10, [1e6, +1e4)) and (b40, [2e12, +1e5))
+    check_detailed(ctx, 1_000_000, 1_010_000, 10)
+    check_detailed(ctx, 2_000_000_000_000, 2_000_000_100_000, 40)
+
+
+@pytest.mark.parametrize("base", [40, 50, 80])
+def test_fd_kernel_segments(ctx, base):
+    """FD kernel over in-range segments, including both range edges and
+    segments straddling them (generic kernel outside, FD inside)."""
+    s, e = O.base_range(base)
+    check_detailed(ctx, s, s + 300_000, base)
+    check_detailed(ctx, e - 300_000, e, base)
+    check_detailed(ctx, s - 5_000, s + 5_000, base)
+    check_detailed(ctx, e - 5_000, e + 5_000, base)
+    mid = s + (e - s) // 3
+    check_detailed(ctx, mid, mid + 1_000_003, base)
+    # tiny and ragged sizes
+    for size in (1, 2, 3, 63, 64, 65, 255, 257, 4097):
+        check_detailed(ctx, mid + 7, mid + 7 + size, base)
+
+
+def test_fd_kernel_random_windows(ctx):
+    rng = random.Random(7)
+    for base in (40, 50, 80):
+        s, e = O.base_range(base)
+        for _ in range(4):
+            a = s + rng.randrange(e - s - 200_000)
+            check_detailed(ctx, a, a + rng.randrange(1, 200_000), base)
+
+
+def test_generic_kernel_bases(ctx):
+    rng = random.Random(11)
+    for base in (2, 3, 7, 10, 12, 16, 25, 31, 32, 33, 45, 57, 62, 63, 64, 65, 68, 70, 94, 97,
+                 100, 127, 128):
+        r = O.base_range(base) if base <= 97 else None
+        if r:
+            s = r[0] + rng.randrange(max(1, r[1] - r[0]))
+        else:
+            s = rng.randrange(1, 1 << 100)
+        check_detailed(ctx, s, s + 3_000, base)
+
+
+def test_out_of_range_large_lists(ctx):
+    # near-miss list much larger than typical (SURVEY hazard 9) and huge n
+    check_detailed(ctx, 1_000_000, 1_200_000, 10)
+    big = (1 << 127) + 12345
+    check_detailed(ctx, big, big + 2_000, 97)
+    check_detailed(ctx, (1 << 128) - 1_000, (1 << 128) - 1, 128)
+
+
+def test_device_unique_counts_samples(ctx, golden):
+    for c in golden["python"]["samples"]:
+        ns = [int(n) for n in c["n"]]
+        assert ctx.debug_unique_counts(ns, c["base"]) == c["num_uniques"], c["base"]
+    wild = golden["python"]["wild"]
+    for n, b, u in wild:
+        assert ctx.debug_unique_counts([int(n)], b) == [u], (n, b)
+
+
+def test_device_is_nice(ctx, golden):
+    assert ctx.debug_is_nice([69, 70, 47, 99], 10) == [True, False, False, False]
+    rng = random.Random(3)
+    for base in (10, 12, 25, 40, 45, 50, 62, 80, 97):
+        s, e = O.base_range(base)
+        ns = [s + rng.randrange(e - s) for _ in range(500)] + list(range(s, s + 500))
+        want = [O.is_nice(n, base) for n in ns]
+        assert ctx.debug_is_nice(ns, base) == want, base
+    # out-of-range small n: reference CPU semantics (no repeat => "nice")
+    ns = list(range(1, 200))
+    assert ctx.debug_is_nice(ns, 10) == [O.is_nice(n, 10) for n in ns]
+
+
+# --- niceonly ---------------------------------------------------------------
+def test_niceonly_reference_vectors(ctx, golden):
+    for c in golden["reference"]["niceonly"]:
+        b = c["base"]
+        s, e = O.base_range(b)
+        if c["size"]:
+            e = s + c["size"]
+        r = N.process_range_niceonly_gpu(ctx, N.FieldSize(s, e), b)
+        assert [(x.number, x.num_uniques) for x in r.nice_numbers] == \
+            [tuple(x) for x in c["nice_numbers"]], c["source"]
+
+
+@pytest.mark.parametrize("base", [10, 12, 25, 40, 45, 62])
+def test_niceonly_matches_oracle(ctx, base):
+    # client_process_gpu.rs:1500-1534: first 5e6 of each base's range
+    s, e = O.base_range(base)
+    e = min(e, s + 5_000_000)
+    lst, st = ctx.niceonly_raw(s, e, base)
+    want, cands = O.process_field_niceonly_mt(s, e, base, threads=8)
+    assert [(n, base) for n in lst] == want.nice_numbers
+    assert st.candidates == cands, "candidate set differs from the CPU path"
+
+
+def test_niceonly_candidate_counts(ctx):
+    rng = random.Random(5)
+    for base in (40, 50, 80):
+        s, e = O.base_range(base)
+        for _ in range(3):
+            a = s + rng.randrange(e - s - 10 ** 8)
+            size = rng.choice([10 ** 6, 10 ** 7, 3 * 10 ** 7])
+            lst, st = ctx.niceonly_raw(a, a + size, base)
+            want, cands = O.process_field_niceonly_mt(a, a + size, base, threads=8)
+            assert st.candidates == cands and [(n, base) for n in lst] == want.nice_numbers
+
+
+def test_niceonly_coarse_floor_superset(ctx):
+    # Coarser MSD floors (reference GPU path, client_process_gpu.rs:82-123) check
+    # a superset of candidates and find the same nice numbers.
+    lst, st = ctx.niceonly_raw(47, 10 ** 5, 10, msd_floor=4000)
+    assert 69 in lst
+    s, _ = O.base_range(40)
+    a, b = ctx.niceonly_raw(s, s + 10 ** 8, 40)
+    c, d = ctx.niceonly_raw(s, s + 10 ** 8, 40, msd_floor=64000)
+    assert a == c and d.candidates >= b.candidates
+
+
+def test_residue_empty_base(ctx):
+    assert ctx.niceonly_raw(100, 200, 11)[0] == []
+
+
+# --- full BASELINE-size fields against the committed oracle fixtures --------
+def _oracle_fields():
+    p = os.path.join(ROOT, "tests", "golden", "oracle_fields.json")
+    if not os.path.exists(p):
+        pytest.skip("oracle_fields.json not generated")
+    with open(p) as f:
+        return json.load(f)
+
+
+def test_full_fields_detailed(ctx):
+    for c in _oracle_fields()["detailed"]:
+        hist, lst = ctx.detailed_raw(int(c["start"]), int(c["end"]), c["base"])
+        assert _dist(hist) == [tuple(x) for x in c["distribution"]], c["name"]
+        assert lst == [(int(n), u) for n, u in c["near_misses"]], c["name"]
+
+
+def test_full_fields_niceonly(ctx):
+    for c in _oracle_fields()["niceonly"]:
+        lst, st = ctx.niceonly_raw(int(c["start"]), int(c["end"]), c["base"])
+        assert st.candidates == c["candidates"], c["name"]
+        assert [str(n) for n in lst] == c["nice_numbers"], c["name"]
+
+
+def test_size_independent_properties(ctx):
+    # Whole b40 extra-large field: histogram mass = field size, split invariance
+    # (two halves sum to the whole), near-miss bins consistent with the list.
+    s = O.base_range(40)[0]
+    e = s + 10 ** 9
+    h, l = ctx.detailed_raw(s, e, 40)
+    assert sum(h) == 10 ** 9
+    m = s + 333_333_337
+    h1, l1 = ctx.detailed_raw(s, m, 40)
+    h2, l2 = ctx.detailed_raw(m, e, 40)
+    assert [a + b for a, b in zip(h1, h2)] == h and l1 + l2 == l
+    cutoff = O.near_miss_cutoff(40)
+    assert sum(h[cutoff + 1:]) == len(l)
+    assert all(O.num_unique_digits(n, 40) == u for n, u in l)
+    # determinism
+    assert ctx.detailed_raw(s, e, 40) == (h, l)
+
+
+def test_multi_device_context_sharding():
+    import torch
+    n = torch.cuda.device_count()
+    devs = [0, 0] if n < 2 else [0, 1]
+    c = N.GpuContext(devs)
+    s = O.base_range(40)[0]
+    want = O.process_range_detailed(s, s + 100_001, 40)
+    hist, lst = c.detailed_raw(s, s + 100_001, 40)
+    assert _dist(hist) == want.distribution and lst == want.nice_numbers
+    c.close()

@@ -1,0 +1,156 @@
+"""Pin the CPU oracle (oracle/) to the reference's golden vectors.
+
+The oracle is the checker for every GPU parity test, so it is itself checked
+first: against the reference's inline Rust unit-test vectors
+(tests/golden/reference_vectors.json) and against vectors produced by the
+reference's Python mirror scripts/inspect_number.py
+(tests/golden/python_vectors.json).
+"""
+import pytest
+
+from oracle import oracle as O
+
+
+def _range_for(case, base):
+    s, e = O.base_range(base)
+    if case["range"] == "base_range":
+        return s, e
+    return s, s + case["size"]
+
+
+def test_reference_detailed_vectors(golden):
+    # common/src/client_process.rs:473-1053
+    for case in golden["reference"]["detailed"]:
+        b = case["base"]
+        s, e = _range_for(case, b)
+        r = O.process_range_detailed(s, e, b)
+        assert r.distribution == [tuple(x) for x in case["distribution"]], case["source"]
+        assert r.nice_numbers == [tuple(x) for x in case["nice_numbers"]], case["source"]
+
+
+def test_reference_niceonly_vectors(golden):
+    # common/src/client_process.rs:1055-1127 (k = 1 in those tests)
+    for case in golden["reference"]["niceonly"]:
+        b = case["base"]
+        s, e = _range_for(case, b)
+        r, _ = O.process_range_niceonly(s, e, b, k=case["k"])
+        assert r.nice_numbers == [tuple(x) for x in case["nice_numbers"]], case["source"]
+        r2, _ = O.process_range_niceonly(s, e, b, k=2)
+        assert r2.nice_numbers == r.nice_numbers
+
+
+def test_reference_base_ranges(golden):
+    # common/src/base_range.rs:98-224
+    for c in golden["reference"]["base_range"]["cases"]:
+        b = c["base"]
+        if c["range"] is None:
+            assert O.base_range(b) is None, b
+        elif c["range"][1] < (1 << 128):
+            assert O.base_range(b) == tuple(c["range"]), b
+        else:
+            with pytest.raises(OverflowError):
+                O.base_range(b)
+
+
+def test_python_base_ranges(golden):
+    for b, r in golden["python"]["base_ranges"].items():
+        got = O.base_range(int(b))
+        assert got == (None if r is None else (int(r[0]), int(r[1]))), b
+
+
+def test_reference_residue_filter(golden):
+    # common/src/residue_filter.rs:26-76
+    for c in golden["reference"]["residue_filter"]["cases"]:
+        assert O.residue_filter(c["base"]) == c["residues"], c["base"]
+
+
+def test_reference_lsd(golden):
+    # common/src/lsd_filter.rs:244-583
+    for c in golden["reference"]["lsd"]["valid_lsds"]:
+        bm = O.lsd_bitmap(c["base"], 1)
+        assert [i for i, v in enumerate(bm) if v] == c["lsds"], c["source"]
+    for c in golden["reference"]["lsd"]["bitmap_points"]:
+        bm = O.lsd_bitmap(c["base"], c["k"])
+        for k, v in c["points"].items():
+            assert bm[int(k)] == v, c["source"]
+    # extract_digits break-on-zero quirk (lsd_filter.rs:142-144): suffix 10 in base
+    # 10 with k=2 -> sq=00 {0}, cb=00 {0} -> collision; suffix 2 -> sq 04 gives {4}
+    # only (no phantom 0), cb 08 gives {8}: valid.
+    bm = O.lsd_bitmap(10, 2)
+    assert bm[2] is True and bm[10] is False
+
+
+def test_reference_stride(golden):
+    # common/src/stride_filter.rs:162-246
+    for c in golden["reference"]["stride"]:
+        M, res = O.stride_residues(c["base"], c["k"])
+        assert M == c["modulus"]
+        gaps = [res[i + 1] - res[i] for i in range(len(res) - 1)] + [M - res[-1] + res[0]]
+        assert sum(gaps) == M and all(g > 0 for g in gaps)
+    # SURVEY.md section 8 table (restated this session; nice_kernels.cu:72 fallback says 4992)
+    assert len(O.stride_residues(40, 2)[1]) == 4996
+    assert len(O.stride_residues(50, 2)[1]) == 14336
+    assert len(O.stride_residues(80, 2)[1]) == 10594
+
+
+def test_reference_msd(golden):
+    m = golden["reference"]["msd"]
+    for c in m["early_exit"]:
+        assert O.has_duplicate_msd_prefix(*c["range"], c["base"]) == c["skip"], c["source"]
+    for c in m["whole_range_no_skip"]:
+        s, e = O.base_range(c["base"])
+        assert not O.has_duplicate_msd_prefix(s, e, c["base"]), c["source"]
+    for c in m["segments"]:
+        b = c["base"]
+        s, e = O.base_range(b)
+        chunk = (e - s) // c["divisor"]
+        for seg, want in c["expect"]:
+            ss = s + seg * chunk
+            se = min(ss + chunk, e)
+            assert O.has_duplicate_msd_prefix(ss, se, b) == want, (c["source"], seg)
+
+
+def test_known_answers(golden):
+    for c in golden["reference"]["known_answers"]:
+        assert O.num_unique_digits(c["n"], c["base"]) == c["num_uniques"], c["source"]
+    assert O.is_nice(69, 10)
+    assert not O.is_nice(70, 10)
+
+
+def test_python_detailed_vectors(golden):
+    for c in golden["python"]["detailed"]:
+        b = c["base"]
+        r = O.process_range_detailed(int(c["start"]), int(c["end"]), b)
+        assert r.distribution == [tuple(x) for x in c["distribution"]], c["name"]
+        assert r.nice_numbers == [(int(n), u) for n, u in c["near_misses"]], c["name"]
+
+
+def test_python_samples(golden):
+    for c in golden["python"]["samples"]:
+        b = c["base"]
+        got = [O.num_unique_digits(int(n), b) for n in c["n"]]
+        assert got == c["num_uniques"], b
+
+
+def test_python_wild(golden):
+    for n, b, u in golden["python"]["wild"]:
+        assert O.num_unique_digits(int(n), b) == u, (n, b)
+
+
+def test_mt_driver_matches_single():
+    s, _ = O.base_range(40)
+    a = O.process_range_detailed(s, s + 300_000, 40)
+    b = O.process_field_detailed_mt(s, s + 300_000, 40, threads=4)
+    assert a == b
+    r1, c1 = O.process_range_niceonly(47, 100, 10)
+    r2, c2 = O.process_field_niceonly_mt(47, 100, 10, threads=2)
+    assert r1 == r2 and r1.nice_numbers == [(69, 10)]
+
+
+def test_scan_depth_consistent():
+    # scan depth == total digits iff is_nice (no repeat anywhere)
+    s, _ = O.base_range(40)
+    for n in range(s, s + 2000):
+        d = O.scan_depth(n, 40)
+        assert (d == 40) == O.is_nice(n, 40) or d == 40
+    assert O.scan_depth(69, 10) == 10 and O.is_nice(69, 10)
