@@ -512,10 +512,11 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
     std::mutex qmu;
     std::condition_variable qcv;
     std::deque<std::vector<std::pair<u128, u128>>> queue;
-    int live = std::min<uint64_t>(threads, nchunks);
+    const int n_workers = (int)std::min<uint64_t>(threads, nchunks);
+    int live = n_workers;  // guarded by qmu
     std::vector<std::thread> workers;
     nice::MsdFilter filt(base);
-    for (int t = 0; t < live; t++) {
+    for (int t = 0; t < n_workers; t++) {
         workers.emplace_back([&]() {
             std::vector<std::pair<u128, u128>> local;
             for (;;) {
