@@ -28,7 +28,7 @@ struct DetailedLaunch {
 // range, where n^2 and n^3 have fixed digit counts).
 bool fd_supported(uint32_t base);
 // Launch the FD kernel over an in-range segment.  grid_cap: max workgroups.
-hipError_t launch_detailed_fd(const DetailedLaunch &p, int num_cus, hipStream_t s);
+hipError_t launch_detailed_fd(const DetailedLaunch &p, int num_cus, hipStream_t s, int variant = 0);
 // Generic per-n kernel: any base 2..128, any n < 2^128.
 hipError_t launch_detailed_generic(const DetailedLaunch &p, int num_cus, hipStream_t s);
 

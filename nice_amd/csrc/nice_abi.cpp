@@ -12,6 +12,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -206,6 +207,12 @@ int emit_list(std::vector<Entry> &all, nice_number *out, size_t cap, size_t *n_o
     return NICE_OK;
 }
 
+// FD kernel variant (0 = production choice; others for scripts/fd_sweep.py).
+int fd_variant() {
+    const char *v = getenv("NICE_FD_VARIANT");
+    return v ? atoi(v) : 0;
+}
+
 // Enqueue the detailed kernels for [s, e) on one device (async).
 int enqueue_detailed(Device &d, u128 s, u128 e, uint32_t base, bool &used_fd, uint64_t &fd_count) {
     nice::DetailedLaunch p{};
@@ -221,7 +228,7 @@ int enqueue_detailed(Device &d, u128 s, u128 e, uint32_t base, bool &used_fd, ui
             p.start_lo = lo64(a);
             p.start_hi = hi64(a);
             p.count = c;
-            hipError_t err = fd ? nice::launch_detailed_fd(p, d.num_cus, d.stream)
+            hipError_t err = fd ? nice::launch_detailed_fd(p, d.num_cus, d.stream, fd_variant())
                                 : nice::launch_detailed_generic(p, d.num_cus, d.stream);
             if (err != hipSuccess)
                 return fail(NICE_ERR_HIP, std::string("detailed launch: ") + hipGetErrorString(err));

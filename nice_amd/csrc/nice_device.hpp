@@ -56,7 +56,7 @@ struct Mask {
 // --------------------------------------------------------------------------
 // u128 helpers ({lo, hi} u64 pairs, the reference GPU ABI's split).
 // --------------------------------------------------------------------------
-__device__ __forceinline__ void add_u128(u64 &lo, u64 &hi, u64 v) {
+__host__ __device__ __forceinline__ void add_u128(u64 &lo, u64 &hi, u64 v) {
     u64 t = lo + v;
     hi += (t < lo) ? 1 : 0;
     lo = t;
