@@ -45,6 +45,30 @@ def parse():
     return p.parse_args()
 
 
+def rank_field(base_start: int, rank: int):
+    """Weak scaling: rank r owns the r-th consecutive 1e9 field of base 40."""
+    start = base_start + rank * FIELD_SIZE
+    return start, start + FIELD_SIZE
+
+
+def timed(step, steps: int, sync, dist=None):
+    """Barrier + device sync on both sides of exactly `steps` steps; returns the
+    max elapsed seconds over ranks (all_reduce MAX)."""
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
 def cpu_threads():
     for k in ("OMP_NUM_THREADS", "MAX_JOBS"):
         if os.environ.get(k, "").isdigit():
@@ -97,11 +121,12 @@ def main():
 
     ctx = N.GpuContext([local])
     br = N.get_base_range_u128(BASE)
-    start = br.range_start + rank * FIELD_SIZE
-    end = start + FIELD_SIZE
+    start, end = rank_field(br.range_start, rank)
     assert end <= br.range_end
 
     def barrier_sync():
+        # Every library call is synchronous (it returns host results), so the
+        # device is idle here; the torch sync/barrier line the ranks up.
         if dist is not None:
             import torch
             torch.cuda.synchronize()
@@ -128,17 +153,7 @@ def main():
     for _ in range(args.warmup):
         step()
     det_ms.clear(), nice_ms.clear(), kern_ms.clear()
-    barrier_sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier_sync()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed(step, args.steps, barrier_sync, dist)
 
     modes = 2 if args.mode == "both" else 1
     total_numbers = modes * FIELD_SIZE * world * args.steps

@@ -10,6 +10,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <memory>
+#include <utility>
 #include <vector>
 
 namespace nice {
@@ -202,13 +204,31 @@ struct StrideTable {
 // ---------------------------------------------------------------------------
 
 // Digits (least significant first) of a value held in u32 words, via chunks of
-// D = b^E < 2^32.
+// D = b^E < 2^32.  BP supplies b, D, E: compile-time (CtBase, divisions become
+// multiply-high sequences) or run-time (RtBase).
 struct DigitBuf {
     uint8_t d[400];
     int n;
 };
 
-inline void digits_of(uint32_t *w, int nw, uint32_t b, uint32_t D, uint32_t E, DigitBuf &out) {
+struct RtBase {
+    uint32_t b, D, E;
+    explicit RtBase(uint32_t base) : b(base), D(1), E(0) {
+        while ((uint64_t)D * b < (1ull << 32)) {
+            D *= b;
+            E++;
+        }
+    }
+};
+template <uint32_t BASE>
+struct CtBase {
+    static constexpr uint32_t b = BASE;
+    static constexpr uint32_t E = []() { uint32_t e = 0; uint64_t d = 1; while (d * BASE < (1ull << 32)) { d *= BASE; e++; } return e; }();
+    static constexpr uint32_t D = []() { uint64_t d = 1; while (d * BASE < (1ull << 32)) d *= BASE; return (uint32_t)d; }();
+};
+
+template <class BP>
+inline void digits_of(uint32_t *w, int nw, const BP &bp, DigitBuf &out) {
     out.n = 0;
     int top = nw - 1;
     while (top >= 0 && w[top] == 0) top--;
@@ -216,56 +236,54 @@ inline void digits_of(uint32_t *w, int nw, uint32_t b, uint32_t D, uint32_t E, D
         uint64_t rem = 0;
         for (int i = top; i >= 0; i--) {
             uint64_t cur = (rem << 32) | w[i];
-            w[i] = (uint32_t)(cur / D);
-            rem = cur % D;
+            w[i] = (uint32_t)(cur / bp.D);
+            rem = cur % bp.D;
         }
         while (top >= 0 && w[top] == 0) top--;
         uint32_t c = (uint32_t)rem;
         if (top >= 0) {
-            for (uint32_t q = 0; q < E; q++) {
-                out.d[out.n++] = (uint8_t)(c % b);
-                c /= b;
+            for (uint32_t q = 0; q < bp.E; q++) {
+                out.d[out.n++] = (uint8_t)(c % bp.b);
+                c /= bp.b;
             }
         } else {
             while (c) {
-                out.d[out.n++] = (uint8_t)(c % b);
-                c /= b;
+                out.d[out.n++] = (uint8_t)(c % bp.b);
+                c /= bp.b;
             }
         }
     }
 }
 
-struct MsdFilter {
-    uint32_t b, D, E;
-    explicit MsdFilter(uint32_t base) : b(base), D(1), E(0) {
-        while ((uint64_t)D * b < (1ull << 32)) {
-            D *= b;
-            E++;
-        }
-    }
+template <class BP>
+struct MsdFilterT {
+    BP bp;
+    explicit MsdFilterT(const BP &p) : bp(p) {}
 
-    // n^2 and n^3 of x as u32 words.
+    // n^2 and n^3 of x as u32 words (only the words that can be non-zero).
     static void powers(u128 x, uint32_t sq[8], uint32_t cu[12]) {
         uint32_t n[4] = {(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
+        int nn = 4;
+        while (nn > 1 && n[nn - 1] == 0) nn--;
         for (int i = 0; i < 8; i++) sq[i] = 0;
-        for (int i = 0; i < 4; i++) {
+        for (int i = 0; i < nn; i++) {
             uint64_t c = 0;
-            for (int j = 0; j < 4; j++) {
+            for (int j = 0; j < nn; j++) {
                 uint64_t t = (uint64_t)n[i] * n[j] + sq[i + j] + c;
                 sq[i + j] = (uint32_t)t;
                 c = t >> 32;
             }
-            sq[i + 4] = (uint32_t)c;
+            sq[i + nn] = (uint32_t)c;
         }
         for (int i = 0; i < 12; i++) cu[i] = 0;
-        for (int i = 0; i < 8; i++) {
+        for (int i = 0; i < 2 * nn; i++) {
             uint64_t c = 0;
-            for (int j = 0; j < 4; j++) {
+            for (int j = 0; j < nn; j++) {
                 uint64_t t = (uint64_t)sq[i] * n[j] + cu[i + j] + c;
                 cu[i + j] = (uint32_t)t;
                 c = t >> 32;
             }
-            cu[i + 4] = (uint32_t)c;
+            cu[i + nn] = (uint32_t)c;
         }
     }
 
@@ -302,22 +320,25 @@ struct MsdFilter {
         powers(first, fsq, fcu);
         powers(last, lsq, lcu);
         DigitBuf ds, de, cs, ce;
-        digits_of(fsq, 8, b, D, E, ds);
-        digits_of(lsq, 8, b, D, E, de);
+        digits_of(fsq, 8, bp, ds);
+        digits_of(lsq, 8, bp, de);
         if (ds.n != de.n) return false;
         const int sp = common_msd(ds, de);
         const uint8_t *sqp = ds.d + (ds.n - sp);
         if (dup(sqp, sp)) return true;
-        digits_of(fcu, 12, b, D, E, cs);
-        digits_of(lcu, 12, b, D, E, ce);
+        digits_of(fcu, 12, bp, cs);
+        digits_of(lcu, 12, bp, ce);
         if (cs.n != ce.n) return false;
         const int cp = common_msd(cs, ce);
         const uint8_t *cup = cs.d + (cs.n - cp);
         if (dup(cup, cp)) return true;
         if (overlap(sqp, sp, cup, cp)) return true;
         // Filter C (k = MSD_LSD_OVERLAP_K_VALUE = 2): uses *first*'s two LSDs.
-        const u128 bk = (u128)b * b;
-        if (first / bk == last / bk) {
+        const uint64_t bk = (uint64_t)bp.b * bp.b;
+        const bool one_class = (uint64_t)(last >> 64) == 0
+                                   ? (uint64_t)first / bk == (uint64_t)last / bk
+                                   : first / bk == last / bk;
+        if (one_class) {
             const int ls = std::min(ds.n, 2), lc = std::min(cs.n, 2);
             if (overlap(sqp, sp, ds.d, ls) || overlap(cup, cp, cs.d, lc) ||
                 overlap(sqp, sp, cs.d, lc) || overlap(cup, cp, ds.d, ls) || dup(ds.d, ls) ||
@@ -345,6 +366,33 @@ struct MsdFilter {
         valid_ranges(s + half, e, depth + 1, floor_size, emit);
     }
 };
+
+// Runtime-dispatched MSD producer: compile-time bases for the benchmark /
+// production bases, a runtime-divisor instance for everything else.
+struct MsdRunner {
+    virtual ~MsdRunner() {}
+    virtual bool skippable(u128 s, u128 e) const = 0;
+    virtual void ranges(u128 s, u128 e, u128 floor_size,
+                        std::vector<std::pair<u128, u128>> &out) const = 0;
+};
+template <class BP>
+struct MsdRunnerT : MsdRunner {
+    MsdFilterT<BP> f;
+    explicit MsdRunnerT(const BP &bp) : f(bp) {}
+    bool skippable(u128 s, u128 e) const override { return f.skippable(s, e); }
+    void ranges(u128 s, u128 e, u128 floor_size,
+                std::vector<std::pair<u128, u128>> &out) const override {
+        f.valid_ranges(s, e, 0, floor_size, [&](u128 a, u128 b) { out.emplace_back(a, b); });
+    }
+};
+inline std::unique_ptr<MsdRunner> make_msd(uint32_t base) {
+    switch (base) {
+    case 40: return std::unique_ptr<MsdRunner>(new MsdRunnerT<CtBase<40>>(CtBase<40>{}));
+    case 50: return std::unique_ptr<MsdRunner>(new MsdRunnerT<CtBase<50>>(CtBase<50>{}));
+    case 80: return std::unique_ptr<MsdRunner>(new MsdRunnerT<CtBase<80>>(CtBase<80>{}));
+    default: return std::unique_ptr<MsdRunner>(new MsdRunnerT<RtBase>(RtBase(base)));
+    }
+}
 
 // Reference client chunking (client/src/main.rs:158-168):
 // 1e6 * clamp(ceil(size / (1e6 * 1e5)), 1, 1000).

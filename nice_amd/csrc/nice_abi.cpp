@@ -437,23 +437,21 @@ int nice_debug_is_nice(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t count, u
 
 int nice_msd_skippable(uint64_t slo, uint64_t shi, uint64_t elo, uint64_t ehi, uint32_t base) {
     if (base < 2 || base > 128 || mk(slo, shi) >= mk(elo, ehi)) return fail(NICE_ERR_INVALID, "bad args");
-    return nice::MsdFilter(base).skippable(mk(slo, shi), mk(elo, ehi)) ? 1 : 0;
+    return nice::make_msd(base)->skippable(mk(slo, shi), mk(elo, ehi)) ? 1 : 0;
 }
 
 int nice_msd_valid_ranges(uint64_t slo, uint64_t shi, uint64_t elo, uint64_t ehi, uint32_t base,
                           uint64_t floor_size, uint64_t *out, size_t cap, size_t *n_out) {
     if (base < 2 || base > 128 || mk(slo, shi) >= mk(elo, ehi)) return fail(NICE_ERR_INVALID, "bad args");
-    nice::MsdFilter f(base);
-    size_t n = 0;
-    f.valid_ranges(mk(slo, shi), mk(elo, ehi), 0, floor_size, [&](u128 a, u128 b) {
-        if (n < cap) {
-            out[4 * n] = lo64(a);
-            out[4 * n + 1] = hi64(a);
-            out[4 * n + 2] = lo64(b);
-            out[4 * n + 3] = hi64(b);
-        }
-        n++;
-    });
+    std::vector<std::pair<u128, u128>> rs;
+    nice::make_msd(base)->ranges(mk(slo, shi), mk(elo, ehi), floor_size, rs);
+    size_t n = rs.size();
+    for (size_t i = 0; i < n && i < cap; i++) {
+        out[4 * i] = lo64(rs[i].first);
+        out[4 * i + 1] = hi64(rs[i].first);
+        out[4 * i + 2] = lo64(rs[i].second);
+        out[4 * i + 3] = hi64(rs[i].second);
+    }
     *n_out = n;
     return n > cap ? fail(NICE_ERR_CAPACITY, "range list exceeds capacity") : NICE_OK;
 }
@@ -522,7 +520,7 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
     const int n_workers = (int)std::min<uint64_t>(threads, nchunks);
     int live = n_workers;  // guarded by qmu
     std::vector<std::thread> workers;
-    nice::MsdFilter filt(base);
+    std::unique_ptr<nice::MsdRunner> filt = nice::make_msd(base);
     for (int t = 0; t < n_workers; t++) {
         workers.emplace_back([&]() {
             std::vector<std::pair<u128, u128>> local;
@@ -531,8 +529,7 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
                 if (i >= nchunks) break;
                 u128 cs = s + (u128)i * chunk;
                 u128 ce = std::min(e, cs + chunk);
-                filt.valid_ranges(cs, ce, 0, floor_size,
-                                  [&](u128 a, u128 b) { local.emplace_back(a, b); });
+                filt->ranges(cs, ce, floor_size, local);
                 if (local.size() >= 4096) {
                     std::lock_guard<std::mutex> g(qmu);
                     queue.push_back(std::move(local));
