@@ -42,6 +42,8 @@ def parse():
                    help="target CPU work for the bounded cpu_baseline sample")
     p.add_argument("--mode", choices=["both", "detailed", "niceonly"], default="both")
     p.add_argument("--msd-floor", type=int, default=0, help="0 = reference CPU-path floor 250")
+    p.add_argument("--msd-where", choices=["auto", "host", "device"], default="auto",
+                   help="niceonly MSD filter placement (same candidate set either way)")
     return p.parse_args()
 
 
@@ -146,7 +148,8 @@ def main():
             assert sum(hist) == FIELD_SIZE
         if args.mode in ("both", "niceonly"):
             t = time.perf_counter()
-            _, st = ctx.niceonly_raw(start, end, BASE, msd_floor=args.msd_floor)
+            _, st = ctx.niceonly_raw(start, end, BASE, msd_floor=args.msd_floor,
+                                     msd_where=args.msd_where)
             nice_ms.append((time.perf_counter() - t) * 1e3)
             last_nice_stats = st
 
@@ -182,6 +185,7 @@ def main():
             "base": BASE, "field_start": start - rank * FIELD_SIZE, "field_size": FIELD_SIZE,
             "mode": args.mode,
             "niceonly_msd_floor": args.msd_floor or 250,
+            "niceonly_msd_where": args.msd_where,
             "niceonly_chunking": "reference client (1e6 * clamp(ceil(size/1e11),1,1000))",
             "parallelism": f"weak{world}",
         },

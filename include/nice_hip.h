@@ -69,12 +69,20 @@ int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start
  *   chunk_size MSD chunking of the field; 0 -> reference client rule
  *              1e6 * clamp(ceil(size / 1e11), 1, 1000) (client/src/main.rs:158-168)
  *   threads    host MSD worker threads; 0 -> hardware concurrency
- *   stride_k   LSD digits in the stride table; 0 -> 2 (client/src/main.rs:19)  */
+ *   stride_k   LSD digits in the stride table; 0 -> 2 (client/src/main.rs:19)
+ *   msd_where  where the MSD recursion runs: 0 auto (device for stride_k 2),
+ *              1 host worker threads, 2 device (level-synchronous kernels)
+ * Both MSD placements produce the same candidate set. */
+#define NICE_MSD_AUTO 0
+#define NICE_MSD_HOST 1
+#define NICE_MSD_DEVICE 2
 typedef struct {
     uint64_t msd_floor;
     uint64_t chunk_size;
     int32_t threads;
     uint32_t stride_k;
+    int32_t msd_where;
+    uint32_t reserved;
 } nice_niceonly_opts;
 
 typedef struct {

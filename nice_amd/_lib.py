@@ -48,7 +48,8 @@ class nice_number(ctypes.Structure):
 
 class nice_niceonly_opts(ctypes.Structure):
     _fields_ = [("msd_floor", ctypes.c_uint64), ("chunk_size", ctypes.c_uint64),
-                ("threads", ctypes.c_int32), ("stride_k", ctypes.c_uint32)]
+                ("threads", ctypes.c_int32), ("stride_k", ctypes.c_uint32),
+                ("msd_where", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
 
 
 class nice_niceonly_stats(ctypes.Structure):

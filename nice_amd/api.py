@@ -171,8 +171,9 @@ class GpuContext:
     # -- niceonly -------------------------------------------------------------
     def niceonly_raw(self, start: int, end: int, base: int, msd_floor: int = 0,
                      chunk_size: int = 0, threads: int = 0, stride_k: int = 0,
-                     cap: int = 1 << 16):
-        opts = _lib.nice_niceonly_opts(msd_floor, chunk_size, threads, stride_k)
+                     msd_where: str = "auto", cap: int = 1 << 16):
+        where = {"auto": 0, "host": 1, "device": 2}[msd_where]
+        opts = _lib.nice_niceonly_opts(msd_floor, chunk_size, threads, stride_k, where, 0)
         st = _lib.nice_niceonly_stats()
         while True:
             out = (_lib.nice_number * max(cap, 1))()

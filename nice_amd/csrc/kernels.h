@@ -32,20 +32,54 @@ hipError_t launch_detailed_fd(const DetailedLaunch &p, int num_cus, hipStream_t 
 // Generic per-n kernel: any base 2..128, any n < 2^128.
 hipError_t launch_detailed_generic(const DetailedLaunch &p, int num_cus, hipStream_t s);
 
-// Niceonly: candidates are enumerated on the device from range descriptors.
+// Niceonly.  A "leaf" is one MSD-surviving sub-range in stride-index form:
+// its candidates are n = b0 + ((g0 + j) / R) * M + residues[(g0 + j) % R],
+// j < count (stride_filter.rs:99-155).  Leaves come from the host MSD producer
+// or from the device MSD filter below.
+struct Leaf {
+    uint64_t b0_lo, b0_hi;  // cycle base: range_start - range_start mod M
+    uint32_t g0;            // lower_bound(residues, range_start mod M), in [0, R]
+    uint32_t count;         // candidates in the range
+};
+
 struct NiceonlyLaunch {
-    const uint64_t *b0;       // per range: u128 cycle base (lo, hi pairs) = start - start % M
-    const uint32_t *g0;       // per range: residue-sequence index of the first candidate
-    const uint64_t *prefix;   // per range: exclusive prefix sum of candidate counts (n_ranges+1)
-    uint32_t n_ranges;
-    uint64_t total;           // total candidates = prefix[n_ranges]
-    const uint32_t *residues; // R valid residues mod M, ascending
+    const Leaf *leaves;
+    const uint32_t *n_leaves_dev;  // leaf count on the device (or null: use n_leaves)
+    uint32_t n_leaves;
+    const uint32_t *residues;      // R valid residues mod M, ascending
     uint32_t R, M;
     uint32_t base;
     NumOut out;
 };
 bool niceonly_specialised(uint32_t base);
 hipError_t launch_niceonly(const NiceonlyLaunch &p, int num_cus, hipStream_t s);
+
+// Device MSD filter (msd_prefix_filter.rs:583-658 as a level-synchronous BFS):
+// one lane per node; leaves (already in stride-index form) are appended to
+// `leaves`.  Nodes: {start lo, hi, size, depth}.
+struct MsdNode {
+    uint64_t lo, hi;
+    uint64_t size;
+    uint32_t depth, pad;
+};
+struct MsdLaunch {
+    uint64_t start_lo, start_hi;  // batch start (first chunk)
+    uint64_t batch_size;          // numbers in this batch (<= 2^63)
+    uint64_t chunk;               // MSD chunk size (client rule)
+    uint64_t floor_size;          // recursion floor (250)
+    MsdNode *q[2];                // ping-pong level queues
+    uint32_t *counters;           // [0..23] level sizes, [24] leaves (batch), [25] overflow
+                                  // flag, [26] leaves (sticky), [28..29] u64 candidates,
+                                  // [30..31] u64 numbers inside leaves (sticky)
+    uint32_t q_cap;
+    Leaf *leaves;
+    uint32_t leaf_cap;
+    const uint32_t *residues;
+    uint32_t R, M;
+    uint32_t base;
+};
+// Enqueue the init + 22 level kernels (no host sync).
+hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s);
 
 // Diagnostics used by the parity tests: per-n unique counts / nice flags
 // computed by the same device functions the production kernels use.

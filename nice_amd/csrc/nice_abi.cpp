@@ -52,14 +52,21 @@ constexpr uint32_t kInitialListCap = 1u << 20;  // NEAR_MISS_CAPACITY (client_pr
 constexpr uint32_t kNiceCap = 1u << 16;         // NICE_OUT_CAPACITY (:71)
 constexpr uint32_t kBatchRanges = 1u << 16;     // LAUNCH_BATCH_RANGES (:583)
 
-struct DescBuf {
-    // host pinned staging + device copies for one niceonly launch
-    uint64_t *h_b0 = nullptr, *d_b0 = nullptr;
-    uint32_t *h_g0 = nullptr, *d_g0 = nullptr;
-    uint64_t *h_prefix = nullptr, *d_prefix = nullptr;
+struct LeafBuf {
+    // host pinned staging + device copy of one launch's leaf descriptors
+    nice::Leaf *h = nullptr, *d = nullptr;
     uint32_t cap = 0;
     hipEvent_t done = nullptr;
     bool pending = false;
+};
+
+struct MsdBuf {
+    // device MSD: ping-pong level queues, leaf list, counters (kernels.h)
+    nice::MsdNode *q[2] = {nullptr, nullptr};
+    nice::Leaf *leaves = nullptr;
+    uint32_t *counters = nullptr;  // 32 words
+    uint32_t *h_counters = nullptr;  // pinned
+    uint32_t q_cap = 0, leaf_cap = 0;
 };
 
 struct Device {
@@ -75,8 +82,9 @@ struct Device {
     uint64_t *h_hist = nullptr;   // pinned
     uint32_t *h_count = nullptr;  // pinned
     std::map<uint32_t, uint32_t *> residues;  // base -> device residue table
-    DescBuf desc[2];
+    LeafBuf desc[2];
     int desc_next = 0;
+    MsdBuf msd;
     nice_kernel_stats last{};
 };
 
@@ -115,26 +123,38 @@ int ensure_list(Device &d, uint32_t cap) {
     return NICE_OK;
 }
 
-int ensure_desc(DescBuf &b, uint32_t cap) {
+int ensure_desc(LeafBuf &b, uint32_t cap) {
     if (b.cap >= cap) return NICE_OK;
     if (b.pending) HIPCHK(hipEventSynchronize(b.done));
     b.pending = false;
-    if (b.h_b0) {
-        HIPCHK(hipHostFree(b.h_b0));
-        HIPCHK(hipHostFree(b.h_g0));
-        HIPCHK(hipHostFree(b.h_prefix));
-        HIPCHK(hipFree(b.d_b0));
-        HIPCHK(hipFree(b.d_g0));
-        HIPCHK(hipFree(b.d_prefix));
+    if (b.h) {
+        HIPCHK(hipHostFree(b.h));
+        HIPCHK(hipFree(b.d));
     }
-    HIPCHK(hipHostMalloc(&b.h_b0, (size_t)cap * 16, hipHostMallocDefault));
-    HIPCHK(hipHostMalloc(&b.h_g0, (size_t)cap * 4, hipHostMallocDefault));
-    HIPCHK(hipHostMalloc(&b.h_prefix, (size_t)(cap + 1) * 8, hipHostMallocDefault));
-    HIPCHK(hipMalloc(&b.d_b0, (size_t)cap * 16));
-    HIPCHK(hipMalloc(&b.d_g0, (size_t)cap * 4));
-    HIPCHK(hipMalloc(&b.d_prefix, (size_t)(cap + 1) * 8));
+    HIPCHK(hipHostMalloc(&b.h, (size_t)cap * sizeof(nice::Leaf), hipHostMallocDefault));
+    HIPCHK(hipMalloc(&b.d, (size_t)cap * sizeof(nice::Leaf)));
     if (!b.done) HIPCHK(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
     b.cap = cap;
+    return NICE_OK;
+}
+
+int ensure_msd(Device &d, uint32_t q_cap, uint32_t leaf_cap) {
+    MsdBuf &m = d.msd;
+    if (!m.counters) {
+        HIPCHK(hipMalloc(&m.counters, 32 * 4));
+        HIPCHK(hipHostMalloc(&m.h_counters, 32 * 4, hipHostMallocDefault));
+    }
+    if (m.q_cap < q_cap) {
+        for (auto &q : m.q)
+            if (q) HIPCHK(hipFree(q));
+        for (auto &q : m.q) HIPCHK(hipMalloc(&q, (size_t)q_cap * sizeof(nice::MsdNode)));
+        m.q_cap = q_cap;
+    }
+    if (m.leaf_cap < leaf_cap) {
+        if (m.leaves) HIPCHK(hipFree(m.leaves));
+        HIPCHK(hipMalloc(&m.leaves, (size_t)leaf_cap * sizeof(nice::Leaf)));
+        m.leaf_cap = leaf_cap;
+    }
     return NICE_OK;
 }
 
@@ -163,16 +183,17 @@ void device_free(Device &d) {
     (void)hipStreamSynchronize(d.stream);
     for (auto &kv : d.residues) (void)hipFree(kv.second);
     for (auto &b : d.desc) {
-        if (b.h_b0) {
-            (void)hipHostFree(b.h_b0);
-            (void)hipHostFree(b.h_g0);
-            (void)hipHostFree(b.h_prefix);
-            (void)hipFree(b.d_b0);
-            (void)hipFree(b.d_g0);
-            (void)hipFree(b.d_prefix);
+        if (b.h) {
+            (void)hipHostFree(b.h);
+            (void)hipFree(b.d);
         }
         if (b.done) (void)hipEventDestroy(b.done);
     }
+    for (auto &q : d.msd.q)
+        if (q) (void)hipFree(q);
+    if (d.msd.leaves) (void)hipFree(d.msd.leaves);
+    if (d.msd.counters) (void)hipFree(d.msd.counters);
+    if (d.msd.h_counters) (void)hipHostFree(d.msd.h_counters);
     (void)hipFree(d.d_hist);
     (void)hipFree(d.d_count);
     (void)hipFree(d.d_list_n);
@@ -510,121 +531,198 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
         if (rc) return rc;
     }
 
-    // Producer: worker threads run the MSD filter per chunk and hand the
-    // surviving ranges to this thread in chunk batches.
-    const uint64_t nchunks = (uint64_t)((e - s + chunk - 1) / chunk);
-    std::atomic<uint64_t> next{0};
-    std::mutex qmu;
-    std::condition_variable qcv;
-    std::deque<std::vector<std::pair<u128, u128>>> queue;
-    const int n_workers = (int)std::min<uint64_t>(threads, nchunks);
-    int live = n_workers;  // guarded by qmu
-    std::vector<std::thread> workers;
-    std::unique_ptr<nice::MsdRunner> filt = nice::make_msd(base);
-    for (int t = 0; t < n_workers; t++) {
-        workers.emplace_back([&]() {
-            std::vector<std::pair<u128, u128>> local;
-            for (;;) {
-                uint64_t i = next.fetch_add(1);
-                if (i >= nchunks) break;
-                u128 cs = s + (u128)i * chunk;
-                u128 ce = std::min(e, cs + chunk);
-                filt->ranges(cs, ce, floor_size, local);
-                if (local.size() >= 4096) {
-                    std::lock_guard<std::mutex> g(qmu);
-                    queue.push_back(std::move(local));
-                    local = {};
-                    qcv.notify_one();
-                }
-            }
-            std::lock_guard<std::mutex> g(qmu);
-            if (!local.empty()) queue.push_back(std::move(local));
-            live--;
-            qcv.notify_one();
-        });
-    }
-
-    // Consumer: build descriptors and launch on devices round-robin.
-    int rc = NICE_OK;
-    size_t dev_rr = 0;
-    std::vector<std::pair<u128, u128>> pend;
-    auto flush = [&]() -> int {
-        if (pend.empty()) return NICE_OK;
-        Device &d = ctx->devs[dev_rr++ % ctx->devs.size()];
-        HIPCHK(hipSetDevice(d.id));
-        DescBuf &b = d.desc[d.desc_next];
-        d.desc_next ^= 1;
-        // Descriptor count: one per range, more for ranges holding over 2^30
-        // candidates (the kernel's residue-sequence index is 32-bit).
-        constexpr u128 kPiece = (u128)1 << 30;
-        size_t need = 0;
-        for (auto &pr : pend) {
-            const u128 c = table->index_of(pr.second) - table->index_of(pr.first);
-            need += (size_t)((c + kPiece - 1) / kPiece);
+    // Device MSD: batches of whole client chunks, each run as init + 23
+    // level kernels + the candidate kernel, all stream-ordered (no host sync
+    // until the end).  Batches alternate over the context's devices.
+    auto run_device = [&]() -> int {
+        if (chunk > ((u128)1 << 40)) return fail(NICE_ERR_INVALID, "device MSD: chunk_size too large");
+        const uint64_t cnk = (uint64_t)chunk;
+        const uint64_t nchunks = (uint64_t)((e - s + chunk - 1) / chunk);
+        // Nodes per level and leaves per batch are <= batch / floor + chunks
+        // (every split child holds >= floor numbers); size batches for 2^24.
+        const uint64_t fl = std::min<uint64_t>(floor_size, 1ull << 30);
+        uint64_t cpb = std::max<uint64_t>(1, (fl << 24) / cnk);
+        cpb = std::min(cpb, nchunks);
+        const uint64_t batch_n = cpb * cnk;
+        uint64_t per = std::min<uint64_t>(batch_n / fl + cpb, cpb << 22) + 64;
+        per = std::min<uint64_t>(per, 1ull << 26);
+        for (auto &d : ctx->devs) {
+            HIPCHK(hipSetDevice(d.id));
+            int r = ensure_msd(d, (uint32_t)per, (uint32_t)per);
+            if (r) return r;
+            HIPCHK(hipMemsetAsync(d.msd.counters, 0, 32 * 4, d.stream));
         }
-        int r = ensure_desc(b, (uint32_t)std::max<size_t>(need, 1));
-        if (r) return r;
-        if (b.pending) HIPCHK(hipEventSynchronize(b.done));
-        uint32_t nr = 0;
-        uint64_t total = 0;
-        for (auto &pr : pend) {
-            const u128 i0 = table->index_of(pr.first), i1 = table->index_of(pr.second);
-            st.ranges++;
-            st.range_numbers += (uint64_t)(pr.second - pr.first);
-            for (u128 g = i0; g < i1; g += kPiece) {
-                // candidate g of the global residue sequence: (g / R) * M + res[g % R]
-                const u128 cyc = g / R;
-                const u128 bs = cyc * M;
-                b.h_b0[2 * nr] = lo64(bs);
-                b.h_b0[2 * nr + 1] = hi64(bs);
-                b.h_g0[nr] = (uint32_t)(g - cyc * R);
-                b.h_prefix[nr] = total;
-                total += (uint64_t)std::min<u128>(kPiece, i1 - g);
-                nr++;
-            }
+        const uint64_t nbatches = (nchunks + cpb - 1) / cpb;
+        for (uint64_t bi = 0; bi < nbatches; bi++) {
+            Device &d = ctx->devs[bi % ctx->devs.size()];
+            HIPCHK(hipSetDevice(d.id));
+            const u128 bs = s + (u128)bi * batch_n;
+            const uint64_t bsize = (uint64_t)std::min<u128>(batch_n, e - bs);
+            HIPCHK(hipMemsetAsync(d.msd.counters, 0, 25 * 4, d.stream));
+            nice::MsdLaunch mp{};
+            mp.start_lo = lo64(bs);
+            mp.start_hi = hi64(bs);
+            mp.batch_size = bsize;
+            mp.chunk = cnk;
+            mp.floor_size = floor_size;
+            mp.q[0] = d.msd.q[0];
+            mp.q[1] = d.msd.q[1];
+            mp.counters = d.msd.counters;
+            mp.q_cap = d.msd.q_cap;
+            mp.leaves = d.msd.leaves;
+            mp.leaf_cap = d.msd.leaf_cap;
+            mp.residues = d.residues[base * 8 + k];
+            mp.R = R;
+            mp.M = (uint32_t)M;
+            mp.base = base;
+            hipError_t err = nice::launch_msd_device(mp, d.num_cus, d.stream);
+            if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("msd launch: ") + hipGetErrorString(err));
+            nice::NiceonlyLaunch p{};
+            p.leaves = d.msd.leaves;
+            p.n_leaves_dev = d.msd.counters + 24;
+            p.n_leaves = d.msd.leaf_cap;  // clamp for the device count
+            p.residues = mp.residues;
+            p.R = R;
+            p.M = (uint32_t)M;
+            p.base = base;
+            p.out = nice::NumOut{d.d_list_n, nullptr, d.d_count + 1, d.list_cap};
+            err = nice::launch_niceonly(p, d.num_cus, d.stream);
+            if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("niceonly launch: ") + hipGetErrorString(err));
+            st.launches++;
         }
-        pend.clear();
-        if (!nr) return NICE_OK;
-        b.h_prefix[nr] = total;
-        st.candidates += total;
-        HIPCHK(hipMemcpyAsync(b.d_b0, b.h_b0, (size_t)nr * 16, hipMemcpyHostToDevice, d.stream));
-        HIPCHK(hipMemcpyAsync(b.d_g0, b.h_g0, (size_t)nr * 4, hipMemcpyHostToDevice, d.stream));
-        HIPCHK(hipMemcpyAsync(b.d_prefix, b.h_prefix, (size_t)(nr + 1) * 8, hipMemcpyHostToDevice,
-                              d.stream));
-        nice::NiceonlyLaunch p{};
-        p.b0 = b.d_b0;
-        p.g0 = b.d_g0;
-        p.prefix = b.d_prefix;
-        p.n_ranges = nr;
-        p.total = total;
-        p.residues = d.residues[base * 8 + k];
-        p.R = R;
-        p.M = (uint32_t)M;
-        p.base = base;
-        p.out = nice::NumOut{d.d_list_n, nullptr, d.d_count + 1, d.list_cap};
-        hipError_t err = nice::launch_niceonly(p, d.num_cus, d.stream);
-        if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("niceonly launch: ") + hipGetErrorString(err));
-        HIPCHK(hipEventRecord(b.done, d.stream));
-        b.pending = true;
-        st.launches++;
+        for (auto &d : ctx->devs) {
+            HIPCHK(hipSetDevice(d.id));
+            HIPCHK(hipMemcpyAsync(d.msd.h_counters, d.msd.counters, 32 * 4, hipMemcpyDeviceToHost,
+                                  d.stream));
+            HIPCHK(hipStreamSynchronize(d.stream));
+            const uint32_t *c = d.msd.h_counters;
+            if (c[25])
+                return fail(NICE_ERR_CAPACITY, "device MSD queue overflow (msd_floor too small for "
+                                               "chunk_size); use msd_where = host");
+            uint64_t cand, nums;
+            std::memcpy(&cand, c + 28, 8);
+            std::memcpy(&nums, c + 30, 8);
+            st.ranges += c[26];
+            st.candidates += cand;
+            st.range_numbers += nums;
+        }
         return NICE_OK;
     };
-    for (;;) {
-        std::vector<std::pair<u128, u128>> item;
-        {
-            std::unique_lock<std::mutex> g(qmu);
-            qcv.wait(g, [&] { return !queue.empty() || live == 0; });
-            if (queue.empty() && live == 0) break;
-            item = std::move(queue.front());
-            queue.pop_front();
+
+    const int where = opts ? opts->msd_where : NICE_MSD_AUTO;
+    if (where < NICE_MSD_AUTO || where > NICE_MSD_DEVICE) return fail(NICE_ERR_INVALID, "bad msd_where");
+    const bool on_device = where == NICE_MSD_DEVICE || (where == NICE_MSD_AUTO && k == 2);
+    int rc = NICE_OK;
+    if (on_device) {
+        rc = run_device();
+    } else {
+        // Producer: worker threads run the MSD filter per chunk and hand the
+        // surviving ranges to this thread in chunk batches.
+        const uint64_t nchunks = (uint64_t)((e - s + chunk - 1) / chunk);
+        std::atomic<uint64_t> next{0};
+        std::mutex qmu;
+        std::condition_variable qcv;
+        std::deque<std::vector<std::pair<u128, u128>>> queue;
+        const int n_workers = (int)std::min<uint64_t>(threads, nchunks);
+        int live = n_workers;  // guarded by qmu
+        std::vector<std::thread> workers;
+        std::unique_ptr<nice::MsdRunner> filt = nice::make_msd(base);
+        for (int t = 0; t < n_workers; t++) {
+            workers.emplace_back([&]() {
+                std::vector<std::pair<u128, u128>> local;
+                for (;;) {
+                    uint64_t i = next.fetch_add(1);
+                    if (i >= nchunks) break;
+                    u128 cs = s + (u128)i * chunk;
+                    u128 ce = std::min(e, cs + chunk);
+                    filt->ranges(cs, ce, floor_size, local);
+                    if (local.size() >= 4096) {
+                        std::lock_guard<std::mutex> g(qmu);
+                        queue.push_back(std::move(local));
+                        local = {};
+                        qcv.notify_one();
+                    }
+                }
+                std::lock_guard<std::mutex> g(qmu);
+                if (!local.empty()) queue.push_back(std::move(local));
+                live--;
+                qcv.notify_one();
+            });
         }
-        if (rc) continue;  // drain the producers after a failure
-        pend.insert(pend.end(), item.begin(), item.end());
-        if (pend.size() >= kBatchRanges) rc = flush();
+
+        // Consumer: build descriptors and launch on devices round-robin.
+        size_t dev_rr = 0;
+        std::vector<std::pair<u128, u128>> pend;
+        auto flush = [&]() -> int {
+            if (pend.empty()) return NICE_OK;
+            Device &d = ctx->devs[dev_rr++ % ctx->devs.size()];
+            HIPCHK(hipSetDevice(d.id));
+            LeafBuf &b = d.desc[d.desc_next];
+            d.desc_next ^= 1;
+            // One leaf per range, more for ranges holding over 2^30 candidates
+            // (the kernel's residue-sequence index is 32-bit).
+            constexpr u128 kPiece = (u128)1 << 30;
+            size_t need = 0;
+            for (auto &pr : pend) {
+                const u128 c = table->index_of(pr.second) - table->index_of(pr.first);
+                need += (size_t)((c + kPiece - 1) / kPiece);
+            }
+            int r = ensure_desc(b, (uint32_t)std::max<size_t>(need, 1));
+            if (r) return r;
+            if (b.pending) HIPCHK(hipEventSynchronize(b.done));
+            uint32_t nr = 0;
+            uint64_t total = 0;
+            for (auto &pr : pend) {
+                const u128 i0 = table->index_of(pr.first), i1 = table->index_of(pr.second);
+                st.ranges++;
+                st.range_numbers += (uint64_t)(pr.second - pr.first);
+                for (u128 g = i0; g < i1; g += kPiece) {
+                    // candidate g of the global residue sequence: (g / R) * M + res[g % R]
+                    const u128 cyc = g / R;
+                    const u128 bs = cyc * M;
+                    const uint32_t cnt = (uint32_t)std::min<u128>(kPiece, i1 - g);
+                    b.h[nr++] = nice::Leaf{lo64(bs), hi64(bs), (uint32_t)(g - cyc * R), cnt};
+                    total += cnt;
+                }
+            }
+            pend.clear();
+            if (!nr) return NICE_OK;
+            st.candidates += total;
+            HIPCHK(hipMemcpyAsync(b.d, b.h, (size_t)nr * sizeof(nice::Leaf), hipMemcpyHostToDevice,
+                                  d.stream));
+            nice::NiceonlyLaunch p{};
+            p.leaves = b.d;
+            p.n_leaves_dev = nullptr;
+            p.n_leaves = nr;
+            p.residues = d.residues[base * 8 + k];
+            p.R = R;
+            p.M = (uint32_t)M;
+            p.base = base;
+            p.out = nice::NumOut{d.d_list_n, nullptr, d.d_count + 1, d.list_cap};
+            hipError_t err = nice::launch_niceonly(p, d.num_cus, d.stream);
+            if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("niceonly launch: ") + hipGetErrorString(err));
+            HIPCHK(hipEventRecord(b.done, d.stream));
+            b.pending = true;
+            st.launches++;
+            return NICE_OK;
+        };
+        for (;;) {
+            std::vector<std::pair<u128, u128>> item;
+            {
+                std::unique_lock<std::mutex> g(qmu);
+                qcv.wait(g, [&] { return !queue.empty() || live == 0; });
+                if (queue.empty() && live == 0) break;
+                item = std::move(queue.front());
+                queue.pop_front();
+            }
+            if (rc) continue;  // drain the producers after a failure
+            pend.insert(pend.end(), item.begin(), item.end());
+            if (pend.size() >= kBatchRanges) rc = flush();
+        }
+        for (auto &w : workers) w.join();
+        st.msd_seconds = std::chrono::duration<double>(clock::now() - t0).count();
+        if (!rc) rc = flush();
     }
-    for (auto &w : workers) w.join();
-    st.msd_seconds = std::chrono::duration<double>(clock::now() - t0).count();
-    if (!rc) rc = flush();
     if (rc) return rc;
 
     std::vector<Entry> all;

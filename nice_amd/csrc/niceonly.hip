@@ -1,45 +1,78 @@
-// niceonly.hip -- gfx950 kernel for niceonly field processing.
+// niceonly.hip -- gfx950 kernels for niceonly field processing.
 //
-// Replaces niceonly_ranges_kernel (common/src/cuda/nice_kernels.cu:420-470)
-// and the CPU stride walk it mirrors (common/src/stride_filter.rs:139-155).
+// Replaces niceonly_ranges_kernel (common/src/cuda/nice_kernels.cu:420-470),
+// the CPU stride walk it mirrors (common/src/stride_filter.rs:139-155) and,
+// optionally, the host MSD recursion in front of it
+// (common/src/msd_prefix_filter.rs:382-674).
 //
-// The host MSD-prefix filter (msd_prefix_filter.rs:583-674) emits surviving
-// sub-ranges; the host turns each into a descriptor {B0, g0, prefix}:
-//   B0     = range_start - range_start mod M       (u128, M = (b-1) b^k)
-//   g0     = index of the first valid residue >= range_start mod M
-//   prefix = exclusive prefix sum of the per-range candidate counts.
-// Candidates are flattened across ranges (load-balanced: one lane per
-// candidate, however short the ranges are -- at the CPU path's MSD floor of
-// 250 a range holds ~20 candidates, a third of a 64-lane wave).  Lane c finds
-// its range by binary search over `prefix`, reconstructs
-//   n = B0 + (g / R) * M + residues[g % R],  g = g0 + (c - prefix[r]),
-// and runs the reference's early-exit check (client_process.rs:222-253).
+// niceonly_kernel: wave-level load balancing.  A wave takes 64 leaves (one per
+// lane), scans their candidate counts across the wave, and then walks the
+// packed candidate space 64 at a time: lane k finds its leaf by a 6-step
+// binary search over the wave's exclusive prefix (cross-lane reads, no LDS),
+// rebuilds n = b0 + ((g0 + j) / R) * M + residues[(g0 + j) % R] and runs the
+// reference's early-exit check (client_process.rs:222-253).  A leaf holds ~20
+// candidates at the CPU path's MSD floor of 250 (b40), so one-wave-per-range
+// would leave two thirds of a 64-lane wave idle.
+//
+// msd_level_kernel: the MSD recursion as a level-synchronous BFS.  Every node
+// of level d is one lane: leaf -> stride-index descriptor appended to the leaf
+// list; skippable -> dropped; else two children appended to level d+1.  The
+// recursion is depth-limited (22), so 23 launches per batch, no host sync.
 #include "kernels.h"
 #include "nice_device.hpp"
 
 namespace nice {
 
+typedef unsigned char u8;
+
+// ---------------------------------------------------------------------------
+// Candidate check kernel
+// ---------------------------------------------------------------------------
 template <class G>
 __global__ void __launch_bounds__(256)
 niceonly_kernel(NiceonlyLaunch p, G g) {
-    for (u64 c = (u64)blockIdx.x * 256 + threadIdx.x; c < p.total; c += (u64)gridDim.x * 256) {
-        // largest r with prefix[r] <= c (that range is non-empty)
-        u32 lo = 0, hi = p.n_ranges;
-        while (hi - lo > 1) {
-            u32 mid = (lo + hi) >> 1;
-            if (p.prefix[mid] <= c) lo = mid;
-            else hi = mid;
+    const u32 lane = threadIdx.x & 63;
+    const u32 gwave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const u32 nwaves = (gridDim.x * blockDim.x) >> 6;
+    const u32 n_leaves = p.n_leaves_dev ? min(*p.n_leaves_dev, p.n_leaves) : p.n_leaves;
+    for (u32 base = gwave * 64; base < n_leaves; base += nwaves * 64) {
+        const u32 li = base + lane;
+        Leaf lf{0, 0, 0, 0};
+        if (li < n_leaves) lf = p.leaves[li];
+        // inclusive scan of counts across the wave
+        u32 incl = lf.count;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            u32 v = __shfl_up(incl, o);
+            if (lane >= (u32)o) incl += v;
         }
-        const u32 gi = p.g0[lo] + (u32)(c - p.prefix[lo]);
-        const u32 cyc = gi / p.R;
-        const u32 j = gi - cyc * p.R;
-        u64 n_lo = p.b0[2 * lo], n_hi = p.b0[2 * lo + 1];
-        add_u128(n_lo, n_hi, (u64)cyc * p.M + p.residues[j]);
-        if (is_nice_dev(n_lo, n_hi, g)) {
-            u32 pos = atomicAdd(p.out.count, 1u);
-            if (pos < p.out.cap) {
-                p.out.n[2 * (u64)pos] = n_lo;
-                p.out.n[2 * (u64)pos + 1] = n_hi;
+        const u32 excl = incl - lf.count;
+        const u32 total = __shfl(incl, 63);
+        for (u32 r0 = 0; r0 < total; r0 += 64) {
+            const u32 k = r0 + lane;
+            // largest l with excl_l <= k (uniform 6-step search, all lanes active)
+            u32 lo = 0;
+#pragma unroll
+            for (u32 step = 32; step >= 1; step >>= 1) {
+                const u32 e = __shfl(excl, lo + step);
+                if (lo + step < 64 && e <= k) lo += step;
+            }
+            const u32 j = k - __shfl(excl, lo);
+            const u32 g0 = __shfl(lf.g0, lo);
+            const u64 b0lo = __shfl(lf.b0_lo, lo), b0hi = __shfl(lf.b0_hi, lo);
+            if (k < total) {
+                const u32 gi = g0 + j;
+                const u32 cyc = gi / p.R;
+                const u32 idx = gi - cyc * p.R;
+                u64 n_lo = b0lo, n_hi = b0hi;
+                add_u128(n_lo, n_hi, (u64)cyc * p.M + p.residues[idx]);
+                if (is_nice_dev(n_lo, n_hi, g)) {
+                    u32 pos = atomicAdd(p.out.count, 1u);
+                    if (pos < p.out.cap) {
+                        p.out.n[2 * (u64)pos] = n_lo;
+                        p.out.n[2 * (u64)pos + 1] = n_hi;
+                    }
+                }
             }
         }
     }
@@ -50,10 +83,204 @@ __global__ void is_nice_kernel(const u64 *n_pairs, u32 count, GenericBase g, u32
     if (i < count) out[i] = is_nice_dev(n_pairs[2 * i], n_pairs[2 * i + 1], g) ? 1u : 0u;
 }
 
+// ---------------------------------------------------------------------------
+// Device MSD filter
+// ---------------------------------------------------------------------------
+
+// u128 {lo, hi} divided by a u32 (q written back), returns the remainder.
+__device__ __forceinline__ u32 divmod_u128(u64 &lo, u64 &hi, u32 d) {
+    u32 w[4] = {(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
+    u64 rem = 0;
+#pragma unroll
+    for (int i = 3; i >= 0; i--) {
+        u64 cur = (rem << 32) | w[i];
+        w[i] = (u32)(cur / d);
+        rem = cur - (u64)w[i] * d;
+    }
+    lo = ((u64)w[1] << 32) | w[0];
+    hi = ((u64)w[3] << 32) | w[2];
+    return (u32)rem;
+}
+
+// Digits (LSD first, until zero) of v into out; returns the count.
+template <int NW, class G, int MAXD>
+__device__ __forceinline__ int digits_to(u32 (&v)[NW], const G &g, u8 (&out)[MAXD]) {
+    int n = 0;
+    int top = NW - 1;
+    while (top >= 0 && v[top] == 0) top--;
+    while (top >= 0) {
+        u32 chunk = div_chunk<NW>(v, top, g.D);
+        if (top >= 0) {
+            for (u32 q = 0; q < g.E; q++) {
+                out[n++] = (u8)(chunk % g.base);
+                chunk /= g.base;
+            }
+        } else {
+            while (chunk) {
+                out[n++] = (u8)(chunk % g.base);
+                chunk /= g.base;
+            }
+        }
+    }
+    return n;
+}
+
+__device__ __forceinline__ bool overlaps(const Mask<4> &a, const Mask<4> &b) {
+    return ((a.w[0] & b.w[0]) | (a.w[1] & b.w[1]) | (a.w[2] & b.w[2]) | (a.w[3] & b.w[3])) != 0;
+}
+
+// has_duplicate_msd_prefix (msd_prefix_filter.rs:382-563) on [first, last].
+template <class G, int MAXD>
+__device__ bool msd_skippable(u64 f_lo, u64 f_hi, u64 l_lo, u64 l_hi, const G &g) {
+    u32 fn[4] = {(u32)f_lo, (u32)(f_lo >> 32), (u32)f_hi, (u32)(f_hi >> 32)};
+    u32 ln[4] = {(u32)l_lo, (u32)(l_lo >> 32), (u32)l_hi, (u32)(l_hi >> 32)};
+    u8 dA[MAXD], dB[MAXD];
+    // squares
+    u32 fsq[8], lsq[8];
+    mul_words<4, 4>(fn, fn, fsq);
+    mul_words<4, 4>(ln, ln, lsq);
+    u32 fsq_keep[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) fsq_keep[i] = fsq[i];
+    const int nA = digits_to<8, G, MAXD>(fsq, g, dA);
+    const int nB = digits_to<8, G, MAXD>(lsq, g, dB);
+    if (nA != nB) return false;
+    int sp = 0;
+    while (sp < nA && dA[nA - 1 - sp] == dB[nA - 1 - sp]) sp++;
+    Mask<4> msq;
+    msq.clear();
+    u32 dup = 0;
+    for (int i = nA - sp; i < nA; i++) dup |= msq.test_set(dA[i]);
+    if (dup) return true;
+    const int ls = nA < 2 ? nA : 2;
+    const u8 lsq0 = dA[0], lsq1 = nA > 1 ? dA[1] : 0;
+    // cubes
+    u32 fcu[12], lcu[12];
+    mul_words<8, 4>(fsq_keep, fn, fcu);
+    u32 lsq2[8];
+    mul_words<4, 4>(ln, ln, lsq2);
+    mul_words<8, 4>(lsq2, ln, lcu);
+    const int cA = digits_to<12, G, MAXD>(fcu, g, dA);
+    const int cB = digits_to<12, G, MAXD>(lcu, g, dB);
+    if (cA != cB) return false;
+    int cp = 0;
+    while (cp < cA && dA[cA - 1 - cp] == dB[cA - 1 - cp]) cp++;
+    Mask<4> mcu;
+    mcu.clear();
+    for (int i = cA - cp; i < cA; i++) dup |= mcu.test_set(dA[i]);
+    if (dup) return true;
+    if (overlaps(msq, mcu)) return true;
+    // Filter C (MSD_LSD_OVERLAP_K_VALUE = 2): first / b^2 == last / b^2, with
+    // *first*'s two lowest digits of n^2 and n^3 (msd_prefix_filter.rs:461-559).
+    u64 a_lo = f_lo, a_hi = f_hi, b_lo = l_lo, b_hi = l_hi;
+    divmod_u128(a_lo, a_hi, g.base * g.base);
+    divmod_u128(b_lo, b_hi, g.base * g.base);
+    if (a_lo == b_lo && a_hi == b_hi) {
+        const int lc = cA < 2 ? cA : 2;
+        Mask<4> ms, mc;
+        ms.clear();
+        mc.clear();
+        u32 ds = ms.test_set(lsq0);
+        if (ls > 1) ds |= ms.test_set(lsq1);
+        u32 dc = mc.test_set(dA[0]);
+        if (lc > 1) dc |= mc.test_set(dA[1]);
+        if (overlaps(msq, ms) || overlaps(mcu, mc) || overlaps(msq, mc) || overlaps(mcu, ms) ||
+            ds || dc || overlaps(ms, mc))
+            return true;
+    }
+    return false;
+}
+
+// Stride-index descriptor of [a, a + size), appended if it holds candidates.
+template <class G>
+__device__ void emit_leaf(u64 a_lo, u64 a_hi, u64 size, const MsdLaunch &p) {
+    u64 q_lo = a_lo, q_hi = a_hi;
+    const u32 ra = divmod_u128(q_lo, q_hi, p.M);
+    u64 e_lo = a_lo, e_hi = a_hi;
+    add_u128(e_lo, e_hi, size);
+    u64 qe_lo = e_lo, qe_hi = e_hi;
+    const u32 re = divmod_u128(qe_lo, qe_hi, p.M);
+    auto lower_bound = [&](u32 x) {
+        u32 lo = 0, hi = p.R;
+        while (lo < hi) {
+            u32 mid = (lo + hi) >> 1;
+            if (p.residues[mid] < x) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    };
+    const u32 g0 = lower_bound(ra), g1 = lower_bound(re);
+    // cycles between the two ends (< 2^64 / M for any batch)
+    const u64 dcyc = qe_lo - q_lo;
+    const u64 count = dcyc * p.R + g1 - g0;
+    if (count == 0) return;
+    const u32 pos = atomicAdd(&p.counters[24], 1u);
+    if (pos >= p.leaf_cap || count > 0xffffffffull) {
+        atomicOr(&p.counters[25], 1u);
+        return;
+    }
+    u64 b0_lo = a_lo, b0_hi = a_hi;
+    // b0 = a - ra  (u128 minus u32)
+    b0_hi -= (b0_lo < ra) ? 1 : 0;
+    b0_lo -= ra;
+    p.leaves[pos] = Leaf{b0_lo, b0_hi, g0, (u32)count};
+    atomicAdd(&p.counters[26], 1u);
+    atomicAdd((unsigned long long *)(p.counters + 28), (unsigned long long)count);
+    atomicAdd((unsigned long long *)(p.counters + 30), (unsigned long long)size);
+}
+
+__global__ void msd_init_kernel(MsdLaunch p) {
+    const u64 nchunks = (p.batch_size + p.chunk - 1) / p.chunk;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nchunks;
+         i += (u64)gridDim.x * blockDim.x) {
+        u64 lo = p.start_lo, hi = p.start_hi;
+        add_u128(lo, hi, i * p.chunk);
+        const u64 size = (p.batch_size - i * p.chunk) < p.chunk ? (p.batch_size - i * p.chunk) : p.chunk;
+        p.q[0][i] = MsdNode{lo, hi, size, 0u, 0u};
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) p.counters[0] = (u32)nchunks;
+}
+
+template <class G, int MAXD>
+__global__ void __launch_bounds__(256)
+msd_level_kernel(MsdLaunch p, u32 level, G g) {
+    const MsdNode *qin = p.q[level & 1];
+    MsdNode *qout = p.q[(level + 1) & 1];
+    const u32 n_in = p.counters[level];
+    for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n_in; i += gridDim.x * blockDim.x) {
+        const MsdNode nd = qin[i];
+        bool leaf = level >= 22 || nd.size <= p.floor_size;
+        if (!leaf) {
+            u64 l_lo = nd.lo, l_hi = nd.hi;
+            add_u128(l_lo, l_hi, nd.size - 1);
+            if (nd.size != 1 && msd_skippable<G, MAXD>(nd.lo, nd.hi, l_lo, l_hi, g)) continue;
+            leaf = nd.size < 2 * p.floor_size;
+        }
+        if (leaf) {
+            emit_leaf<G>(nd.lo, nd.hi, nd.size, p);
+        } else {
+            const u64 half = nd.size / 2;
+            const u32 pos = atomicAdd(&p.counters[level + 1], 2u);
+            if (pos + 1 >= p.q_cap) {
+                atomicOr(&p.counters[25], 1u);
+                continue;
+            }
+            u64 m_lo = nd.lo, m_hi = nd.hi;
+            add_u128(m_lo, m_hi, half);
+            qout[pos] = MsdNode{nd.lo, nd.hi, half, level + 1, 0u};
+            qout[pos + 1] = MsdNode{m_lo, m_hi, nd.size - half, level + 1, 0u};
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host launchers
+// ---------------------------------------------------------------------------
 template <class G>
 static hipError_t launch_nice(const NiceonlyLaunch &p, const G &g, int num_cus, hipStream_t s) {
-    u64 grid = (p.total + 255) / 256;
-    const u64 cap = (u64)num_cus * 16;
+    u64 waves = p.n_leaves_dev ? (u64)num_cus * 32 : ((u64)p.n_leaves + 63) / 64;
+    u64 grid = (waves + 3) / 4;
+    const u64 cap = (u64)num_cus * 8;
     if (grid > cap) grid = cap;
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL(niceonly_kernel<G>, dim3((u32)grid), dim3(256), 0, s, p, g);
@@ -72,12 +299,31 @@ bool niceonly_specialised(uint32_t base) {
 }
 
 hipError_t launch_niceonly(const NiceonlyLaunch &p, int num_cus, hipStream_t s) {
-    if (p.total == 0) return hipSuccess;
+    if (!p.n_leaves_dev && p.n_leaves == 0) return hipSuccess;
     switch (p.base) {
 #define X(b) case b: return launch_nice(p, ConstBase<b>{}, num_cus, s);
         NICE_NICEONLY_BASES(X)
 #undef X
     default: return launch_nice(p, make_generic(p.base), num_cus, s);
+    }
+}
+
+template <class G, int MAXD>
+static hipError_t launch_msd(const MsdLaunch &p, const G &g, int num_cus, hipStream_t s) {
+    hipLaunchKernelGGL(msd_init_kernel, dim3(256), dim3(256), 0, s, p);
+    const u32 grid = (u32)num_cus * 8;
+    for (u32 level = 0; level <= 22; level++)
+        hipLaunchKernelGGL((msd_level_kernel<G, MAXD>), dim3(grid), dim3(256), 0, s, p, level, g);
+    return hipGetLastError();
+}
+
+hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s) {
+    // MAXD: digits of n^3 < 2^384 in the base (floor(log2 b) bits per digit).
+    switch (p.base) {
+    case 40: return launch_msd<ConstBase<40>, 80>(p, ConstBase<40>{}, num_cus, s);
+    case 50: return launch_msd<ConstBase<50>, 80>(p, ConstBase<50>{}, num_cus, s);
+    case 80: return launch_msd<ConstBase<80>, 66>(p, ConstBase<80>{}, num_cus, s);
+    default: return launch_msd<GenericBase, 390>(p, make_generic(p.base), num_cus, s);
     }
 }
 

@@ -142,25 +142,30 @@ def test_niceonly_reference_vectors(ctx, golden):
             [tuple(x) for x in c["nice_numbers"]], c["source"]
 
 
-@pytest.mark.parametrize("base", [10, 12, 25, 40, 45, 62])
-def test_niceonly_matches_oracle(ctx, base):
+MSD_WHERE = ["host", "device"]
+
+
+@pytest.mark.parametrize("where", MSD_WHERE)
+@pytest.mark.parametrize("base", [10, 12, 25, 40, 45, 62, 97])
+def test_niceonly_matches_oracle(ctx, base, where):
     # client_process_gpu.rs:1500-1534: first 5e6 of each base's range
     s, e = O.base_range(base)
     e = min(e, s + 5_000_000)
-    lst, st = ctx.niceonly_raw(s, e, base)
+    lst, st = ctx.niceonly_raw(s, e, base, msd_where=where)
     want, cands = O.process_field_niceonly_mt(s, e, base, threads=8)
     assert [(n, base) for n in lst] == want.nice_numbers
     assert st.candidates == cands, "candidate set differs from the CPU path"
 
 
-def test_niceonly_candidate_counts(ctx):
+@pytest.mark.parametrize("where", MSD_WHERE)
+def test_niceonly_candidate_counts(ctx, where):
     rng = random.Random(5)
     for base in (40, 50, 80):
         s, e = O.base_range(base)
         for _ in range(3):
             a = s + rng.randrange(e - s - 10 ** 8)
             size = rng.choice([10 ** 6, 10 ** 7, 3 * 10 ** 7])
-            lst, st = ctx.niceonly_raw(a, a + size, base)
+            lst, st = ctx.niceonly_raw(a, a + size, base, msd_where=where)
             want, cands = O.process_field_niceonly_mt(a, a + size, base, threads=8)
             assert st.candidates == cands and [(n, base) for n in lst] == want.nice_numbers
 
@@ -174,6 +179,49 @@ def test_niceonly_coarse_floor_superset(ctx):
     a, b = ctx.niceonly_raw(s, s + 10 ** 8, 40)
     c, d = ctx.niceonly_raw(s, s + 10 ** 8, 40, msd_floor=64000)
     assert a == c and d.candidates >= b.candidates
+
+
+def test_niceonly_device_msd_edges(ctx):
+    # Ragged / tiny ranges, custom chunking, deep recursion (floor 1 -> depth
+    # limit 22), chunk boundaries: the device MSD must reproduce the host MSD
+    # candidate set exactly.
+    rng = random.Random(11)
+    cases = []
+    for base in (40, 50, 80, 10, 33):
+        s, e = O.base_range(base)
+        for size in (1, 2, 63, 250, 499, 500, 501, 10 ** 4 + 7):
+            a = s + rng.randrange(max(1, e - s - size))
+            cases.append((base, a, min(e, a + size), {}))
+    s40 = O.base_range(40)[0]
+    cases += [
+        (40, s40 + 12345, s40 + 12345 + 3_000_001, {"chunk_size": 999_983}),
+        (40, s40, s40 + 2_000_000, {"msd_floor": 1}),
+        (40, s40 + 5, s40 + 40_000_000, {"msd_floor": 7, "chunk_size": 5_000_000}),
+        (50, O.base_range(50)[0], O.base_range(50)[0] + 10 ** 7, {"msd_floor": 1000}),
+    ]
+    for base, a, b, kw in cases:
+        h_l, h_st = ctx.niceonly_raw(a, b, base, msd_where="host", **kw)
+        d_l, d_st = ctx.niceonly_raw(a, b, base, msd_where="device", **kw)
+        assert d_l == h_l and d_st.candidates == h_st.candidates, (base, a, b, kw)
+        if not kw:
+            want, cands = O.process_field_niceonly_mt(a, b, base, threads=8)
+            assert d_st.candidates == cands and [(n, base) for n in d_l] == want.nice_numbers
+
+
+def test_niceonly_multi_device_context():
+    import torch
+    n = torch.cuda.device_count()
+    devs = [0, 0] if n < 2 else [0, 1]
+    c = N.GpuContext(devs)
+    s = O.base_range(40)[0]
+    # 3e8 at chunk 1e6, floor 4 -> 5 device-MSD batches alternating over devices
+    for where in MSD_WHERE:
+        lst, st = c.niceonly_raw(s, s + 3 * 10 ** 8, 40, msd_where=where, chunk_size=10 ** 6,
+                                 msd_floor=4)
+        one, st1 = N.GpuContext([0]).niceonly_raw(s, s + 3 * 10 ** 8, 40, msd_where=where,
+                                                  chunk_size=10 ** 6, msd_floor=4)
+        assert lst == one and st.candidates == st1.candidates
+    c.close()
 
 
 def test_residue_empty_base(ctx):
@@ -196,9 +244,10 @@ def test_full_fields_detailed(ctx):
         assert lst == [(int(n), u) for n, u in c["near_misses"]], c["name"]
 
 
-def test_full_fields_niceonly(ctx):
+@pytest.mark.parametrize("where", MSD_WHERE)
+def test_full_fields_niceonly(ctx, where):
     for c in _oracle_fields()["niceonly"]:
-        lst, st = ctx.niceonly_raw(int(c["start"]), int(c["end"]), c["base"])
+        lst, st = ctx.niceonly_raw(int(c["start"]), int(c["end"]), c["base"], msd_where=where)
         assert st.candidates == c["candidates"], c["name"]
         assert [str(n) for n in lst] == c["nice_numbers"], c["name"]
 
