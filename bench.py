@@ -8,9 +8,12 @@ stride candidates), exactly what the reference client does per field
 (client/src/main.rs:120-208, process_range_*_gpu).  Inputs are the field
 bounds only (no host buffers): the kernels derive every n themselves.
 
-Multi-GPU (one process per GPU, torchrun): weak scaling -- rank r processes
-its own consecutive 1e9 field [start + r*1e9, start + (r+1)*1e9) of base 40,
-as independent volunteer claims would; there is no data-path collective.
+Multi-GPU (one process per GPU, torchrun): weak scaling -- N GPUs process one
+N x 1e9 field of base 40, [start, start + N*1e9); rank r takes the r-th
+contiguous 1e9 shard (nice_amd/dist.py).  Per step the shard histograms are
+combined with one RCCL all-reduce (base + 1 u64 bins) and the near-miss / nice
+lists are all-gathered, so every rank ends the step holding the whole field's
+results -- the north star's exchange, inside the timed region.
 Timing: barrier + device sync on both sides of exactly K steps, max over ranks.
 
     python bench.py [--gpus N --steps K --warmup W] [--no-cpu-baseline]
@@ -137,19 +140,35 @@ def main():
 
     det_ms, nice_ms, kern_ms = [], [], []
     last_nice_stats = None
+    from nice_amd import dist as D
+    whole = N.FieldSize(br.range_start, br.range_start + world * FIELD_SIZE)
 
     def step():
         nonlocal last_nice_stats
         if args.mode in ("both", "detailed"):
             t = time.perf_counter()
-            hist, lst = ctx.detailed_raw(start, end, BASE)
+            if dist is None:
+                hist, lst = ctx.detailed_raw(start, end, BASE)
+                mass = sum(hist)
+            else:
+                r = D.process_range_detailed_dist(whole, BASE, ctx=ctx)
+                mass = sum(d.count for d in r.distribution)
             det_ms.append((time.perf_counter() - t) * 1e3)
             kern_ms.append(ctx.kernel_stats().kernel_ms)
-            assert sum(hist) == FIELD_SIZE
+            assert mass == FIELD_SIZE * world
         if args.mode in ("both", "niceonly"):
             t = time.perf_counter()
-            _, st = ctx.niceonly_raw(start, end, BASE, msd_floor=args.msd_floor,
-                                     msd_where=args.msd_where)
+            if dist is None:
+                _, st = ctx.niceonly_raw(start, end, BASE, msd_floor=args.msd_floor,
+                                         msd_where=args.msd_where)
+            else:
+                def shard(s, e, b, chunk):
+                    nonlocal st
+                    lst, st = ctx.niceonly_raw(s, e, b, chunk_size=chunk, msd_floor=args.msd_floor,
+                                               msd_where=args.msd_where)
+                    return lst
+                st = None
+                D.process_range_niceonly_dist(whole, BASE, shard_fn=shard)
             nice_ms.append((time.perf_counter() - t) * 1e3)
             last_nice_stats = st
 
@@ -181,7 +200,8 @@ def main():
         "data": "synthetic (the reference's deterministic benchmark field; n derived on device)",
         "config": {
             "workload": "extra-large: 1e9 @ base 40, detailed + niceonly per step "
-                        "(benchmark.rs:60; rank r takes the r-th consecutive 1e9 field)",
+                        "(benchmark.rs:60); N GPUs: one N x 1e9 field, rank r takes the r-th "
+                        "1e9 shard, histogram all-reduce + list all-gather per step",
             "base": BASE, "field_start": start - rank * FIELD_SIZE, "field_size": FIELD_SIZE,
             "mode": args.mode,
             "niceonly_msd_floor": args.msd_floor or 250,

@@ -46,3 +46,73 @@ def test_two_rank_weak_scaling_plumbing():
     assert f1[1] <= 6_553_600_000_000  # inside base 40's range (base_range.rs:86-87)
     # max over ranks: both ranks report the slower rank's time (2 x 0.1 s)
     assert abs(e0 - e1) < 1e-9 and e0 >= 0.2
+
+
+# --- one field across ranks: histogram all-reduce + list all-gather ----------
+def _oracle_detailed_shard(s, e, base):
+    from oracle import oracle as O
+    r = O.process_range_detailed(s, e, base)
+    hist = [0] * (base + 1)
+    for u, c in r.distribution:
+        hist[u] = c
+    return hist, list(r.nice_numbers)
+
+
+def _oracle_niceonly_shard(s, e, base, chunk):
+    from oracle import oracle as O
+    out = []
+    a = s
+    while a < e:
+        b = min(e, a + chunk)
+        out += [n for n, _ in O.process_range_niceonly(a, b, base)[0].nice_numbers]
+        a = b
+    return out
+
+
+def _field_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from nice_amd import dist as D
+    from nice_amd.types import FieldSize
+    res = {}
+    s40 = 1_916_284_264_916
+    for name, f, b in [("b40", FieldSize(s40, s40 + 200_001), 40),
+                       ("b10_oob", FieldSize(10 ** 6, 10 ** 6 + 10 ** 4), 10)]:
+        r = D.process_range_detailed_dist(f, b, shard_fn=_oracle_detailed_shard)
+        res[name] = ([(d.num_uniques, d.count) for d in r.distribution],
+                     [(n.number, n.num_uniques) for n in r.nice_numbers])
+    r = D.process_range_niceonly_dist(FieldSize(47, 100), 10, shard_fn=_oracle_niceonly_shard)
+    res["nice_b10"] = [(n.number, n.num_uniques) for n in r.nice_numbers]
+    r = D.process_range_niceonly_dist(FieldSize(s40, s40 + 10 ** 6), 40, chunk_size=99_991,
+                                      shard_fn=_oracle_niceonly_shard)
+    res["nice_b40"] = [(n.number, n.num_uniques) for n in r.nice_numbers]
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def test_two_rank_field_sharding_matches_single_process():
+    from oracle import oracle as O
+    from nice_amd import dist as D
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_field_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[0] == out[1]  # every rank holds the whole field's results
+    s40 = 1_916_284_264_916
+    w = O.process_range_detailed(s40, s40 + 200_001, 40)
+    assert out[0]["b40"] == (w.distribution, w.nice_numbers)
+    w = O.process_range_detailed(10 ** 6, 10 ** 6 + 10 ** 4, 10)
+    assert out[0]["b10_oob"] == (w.distribution, w.nice_numbers)
+    assert len(w.nice_numbers) == 5395  # lists gathered in ascending order
+    assert out[0]["nice_b10"] == [(69, 10)]
+    assert out[0]["nice_b40"] == []
+    # shard cuts fall on the whole field's chunk grid
+    assert D.shard_bounds(0, 10 ** 6, 0, 2, 99_991)[1] % 99_991 == 0
+    assert D.shard_bounds(0, 10, 1, 3) == (4, 7)
+    assert D.client_chunk_size(10 ** 9) == 10 ** 6 and D.client_chunk_size(10 ** 13) == 10 ** 8
