@@ -95,10 +95,21 @@ struct ConstBase {
     static constexpr u32 D = []() { u32 d = 1; while ((unsigned long long)d * BASE <= 65535u) d *= BASE; return d; }();
 };
 
+// Index of the highest non-zero word (-1 for zero), static indexing only (a
+// data-dependent index would push the array to scratch memory).
+template <int NW>
+__device__ __forceinline__ int top_word(const u32 (&v)[NW]) {
+    int t = -1;
+#pragma unroll
+    for (int i = 0; i < NW; i++) t = v[i] ? i : t;
+    return t;
+}
+
 // In-place v /= D over 16-bit halves of u32 words [0, top]; returns v % D.
+// D < 2^16, so the quotient loses at most one top word.
 template <int NW>
 __device__ __forceinline__ u32 div_chunk(u32 (&v)[NW], int &top, u32 D) {
-    u32 rem = 0;
+    u32 rem = 0, vt = 0;
 #pragma unroll
     for (int i = NW - 1; i >= 0; i--) {
         if (i > top) continue;
@@ -110,8 +121,9 @@ __device__ __forceinline__ u32 div_chunk(u32 (&v)[NW], int &top, u32 D) {
         u32 ql = cur / D;
         rem = cur - ql * D;
         v[i] = (qh << 16) | ql;
+        if (i == top) vt = v[i];
     }
-    while (top >= 0 && v[top] == 0) top--;
+    top -= (vt == 0) ? 1 : 0;
     return rem;
 }
 
@@ -119,8 +131,7 @@ __device__ __forceinline__ u32 div_chunk(u32 (&v)[NW], int &top, u32 D) {
 // repeated digit (returns false).
 template <int NW, bool STOP, class G>
 __device__ __forceinline__ bool scan_generic(u32 (&v)[NW], const G &g, Mask<4> &m) {
-    int top = NW - 1;
-    while (top >= 0 && v[top] == 0) top--;
+    int top = top_word(v);
     while (top >= 0) {
         u32 chunk = div_chunk<NW>(v, top, g.D);
         u32 dup = 0;

@@ -23,7 +23,6 @@
 
 namespace nice {
 
-typedef unsigned char u8;
 
 // ---------------------------------------------------------------------------
 // Candidate check kernel
@@ -102,90 +101,93 @@ __device__ __forceinline__ u32 divmod_u128(u64 &lo, u64 &hi, u32 d) {
     return (u32)rem;
 }
 
-// Digits (LSD first, until zero) of v into out; returns the count.
-template <int NW, class G, int MAXD>
-__device__ __forceinline__ int digits_to(u32 (&v)[NW], const G &g, u8 (&out)[MAXD]) {
-    int n = 0;
-    int top = NW - 1;
-    while (top >= 0 && v[top] == 0) top--;
-    while (top >= 0) {
-        u32 chunk = div_chunk<NW>(v, top, g.D);
-        if (top >= 0) {
-            for (u32 q = 0; q < g.E; q++) {
-                out[n++] = (u8)(chunk % g.base);
-                chunk /= g.base;
-            }
-        } else {
-            while (chunk) {
-                out[n++] = (u8)(chunk % g.base);
-                chunk /= g.base;
-            }
-        }
-    }
-    return n;
-}
-
 __device__ __forceinline__ bool overlaps(const Mask<4> &a, const Mask<4> &b) {
     return ((a.w[0] & b.w[0]) | (a.w[1] & b.w[1]) | (a.w[2] & b.w[2]) | (a.w[3] & b.w[3])) != 0;
 }
 
+// Common most-significant-digit prefix of x and y (both consumed), in one
+// least-significant-first pass over both, without storing digits: the running
+// mask holds the digits seen since the last position where x and y differed,
+// and is snapshotted at every non-zero digit of x, so after the pass the
+// snapshot is the mask of the common prefix of the two numbers.  Returns false
+// if the digit counts differ; lsd0/lsd1 are x's two lowest digits.
+struct PrefixScan {
+    Mask<4> mask;
+    u32 dup;
+    u32 lsd0, lsd1;
+    int len;
+};
+template <int NW, class G>
+__device__ __forceinline__ bool common_prefix(u32 (&x)[NW], u32 (&y)[NW], const G &g,
+                                              PrefixScan &r) {
+    int tx = top_word(x), ty = top_word(y);
+    Mask<4> cur;
+    cur.clear();
+    r.mask.clear();
+    u32 dup = 0;
+    r.dup = 0;
+    r.lsd0 = r.lsd1 = 0;
+    int pos = 0, lx = 0, ly = 0;
+    while (tx >= 0 || ty >= 0) {
+        u32 cx = tx >= 0 ? div_chunk<NW>(x, tx, g.D) : 0u;
+        u32 cy = ty >= 0 ? div_chunk<NW>(y, ty, g.D) : 0u;
+        for (u32 q = 0; q < g.E; q++, pos++) {
+            const u32 dx = cx % g.base, dy = cy % g.base;
+            cx /= g.base;
+            cy /= g.base;
+            if (pos == 0) r.lsd0 = dx;
+            if (pos == 1) r.lsd1 = dx;
+            if (dx != dy) {
+                cur.clear();
+                dup = 0;
+            } else {
+                dup |= cur.test_set(dx);
+            }
+            if (dx) {
+                lx = pos + 1;
+                r.mask = cur;
+                r.dup = dup;
+            }
+            if (dy) ly = pos + 1;
+        }
+    }
+    r.len = lx;
+    return lx == ly;
+}
+
 // has_duplicate_msd_prefix (msd_prefix_filter.rs:382-563) on [first, last].
-template <class G, int MAXD>
+template <class G>
 __device__ bool msd_skippable(u64 f_lo, u64 f_hi, u64 l_lo, u64 l_hi, const G &g) {
     u32 fn[4] = {(u32)f_lo, (u32)(f_lo >> 32), (u32)f_hi, (u32)(f_hi >> 32)};
     u32 ln[4] = {(u32)l_lo, (u32)(l_lo >> 32), (u32)l_hi, (u32)(l_hi >> 32)};
-    u8 dA[MAXD], dB[MAXD];
-    // squares
     u32 fsq[8], lsq[8];
     mul_words<4, 4>(fn, fn, fsq);
     mul_words<4, 4>(ln, ln, lsq);
-    u32 fsq_keep[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) fsq_keep[i] = fsq[i];
-    const int nA = digits_to<8, G, MAXD>(fsq, g, dA);
-    const int nB = digits_to<8, G, MAXD>(lsq, g, dB);
-    if (nA != nB) return false;
-    int sp = 0;
-    while (sp < nA && dA[nA - 1 - sp] == dB[nA - 1 - sp]) sp++;
-    Mask<4> msq;
-    msq.clear();
-    u32 dup = 0;
-    for (int i = nA - sp; i < nA; i++) dup |= msq.test_set(dA[i]);
-    if (dup) return true;
-    const int ls = nA < 2 ? nA : 2;
-    const u8 lsq0 = dA[0], lsq1 = nA > 1 ? dA[1] : 0;
-    // cubes
     u32 fcu[12], lcu[12];
-    mul_words<8, 4>(fsq_keep, fn, fcu);
-    u32 lsq2[8];
-    mul_words<4, 4>(ln, ln, lsq2);
-    mul_words<8, 4>(lsq2, ln, lcu);
-    const int cA = digits_to<12, G, MAXD>(fcu, g, dA);
-    const int cB = digits_to<12, G, MAXD>(lcu, g, dB);
-    if (cA != cB) return false;
-    int cp = 0;
-    while (cp < cA && dA[cA - 1 - cp] == dB[cA - 1 - cp]) cp++;
-    Mask<4> mcu;
-    mcu.clear();
-    for (int i = cA - cp; i < cA; i++) dup |= mcu.test_set(dA[i]);
-    if (dup) return true;
-    if (overlaps(msq, mcu)) return true;
+    mul_words<8, 4>(fsq, fn, fcu);
+    mul_words<8, 4>(lsq, ln, lcu);
+    PrefixScan sq, cu;
+    if (!common_prefix<8>(fsq, lsq, g, sq)) return false;  // digit counts differ
+    if (sq.dup) return true;
+    if (!common_prefix<12>(fcu, lcu, g, cu)) return false;
+    if (cu.dup) return true;
+    if (overlaps(sq.mask, cu.mask)) return true;
     // Filter C (MSD_LSD_OVERLAP_K_VALUE = 2): first / b^2 == last / b^2, with
     // *first*'s two lowest digits of n^2 and n^3 (msd_prefix_filter.rs:461-559).
     u64 a_lo = f_lo, a_hi = f_hi, b_lo = l_lo, b_hi = l_hi;
     divmod_u128(a_lo, a_hi, g.base * g.base);
     divmod_u128(b_lo, b_hi, g.base * g.base);
     if (a_lo == b_lo && a_hi == b_hi) {
-        const int lc = cA < 2 ? cA : 2;
         Mask<4> ms, mc;
         ms.clear();
         mc.clear();
-        u32 ds = ms.test_set(lsq0);
-        if (ls > 1) ds |= ms.test_set(lsq1);
-        u32 dc = mc.test_set(dA[0]);
-        if (lc > 1) dc |= mc.test_set(dA[1]);
-        if (overlaps(msq, ms) || overlaps(mcu, mc) || overlaps(msq, mc) || overlaps(mcu, ms) ||
-            ds || dc || overlaps(ms, mc))
+        u32 ds = 0, dc = 0;
+        if (sq.len > 0) ds |= ms.test_set(sq.lsd0);
+        if (sq.len > 1) ds |= ms.test_set(sq.lsd1);
+        if (cu.len > 0) dc |= mc.test_set(cu.lsd0);
+        if (cu.len > 1) dc |= mc.test_set(cu.lsd1);
+        if (overlaps(sq.mask, ms) || overlaps(cu.mask, mc) || overlaps(sq.mask, mc) ||
+            overlaps(cu.mask, ms) || ds || dc || overlaps(ms, mc))
             return true;
     }
     return false;
@@ -241,7 +243,7 @@ __global__ void msd_init_kernel(MsdLaunch p) {
     if (blockIdx.x == 0 && threadIdx.x == 0) p.counters[0] = (u32)nchunks;
 }
 
-template <class G, int MAXD>
+template <class G>
 __global__ void __launch_bounds__(256)
 msd_level_kernel(MsdLaunch p, u32 level, G g) {
     const MsdNode *qin = p.q[level & 1];
@@ -253,7 +255,7 @@ msd_level_kernel(MsdLaunch p, u32 level, G g) {
         if (!leaf) {
             u64 l_lo = nd.lo, l_hi = nd.hi;
             add_u128(l_lo, l_hi, nd.size - 1);
-            if (nd.size != 1 && msd_skippable<G, MAXD>(nd.lo, nd.hi, l_lo, l_hi, g)) continue;
+            if (nd.size != 1 && msd_skippable<G>(nd.lo, nd.hi, l_lo, l_hi, g)) continue;
             leaf = nd.size < 2 * p.floor_size;
         }
         if (leaf) {
@@ -308,22 +310,21 @@ hipError_t launch_niceonly(const NiceonlyLaunch &p, int num_cus, hipStream_t s) 
     }
 }
 
-template <class G, int MAXD>
+template <class G>
 static hipError_t launch_msd(const MsdLaunch &p, const G &g, int num_cus, hipStream_t s) {
     hipLaunchKernelGGL(msd_init_kernel, dim3(256), dim3(256), 0, s, p);
     const u32 grid = (u32)num_cus * 8;
     for (u32 level = 0; level <= 22; level++)
-        hipLaunchKernelGGL((msd_level_kernel<G, MAXD>), dim3(grid), dim3(256), 0, s, p, level, g);
+        hipLaunchKernelGGL((msd_level_kernel<G>), dim3(grid), dim3(256), 0, s, p, level, g);
     return hipGetLastError();
 }
 
 hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s) {
-    // MAXD: digits of n^3 < 2^384 in the base (floor(log2 b) bits per digit).
     switch (p.base) {
-    case 40: return launch_msd<ConstBase<40>, 80>(p, ConstBase<40>{}, num_cus, s);
-    case 50: return launch_msd<ConstBase<50>, 80>(p, ConstBase<50>{}, num_cus, s);
-    case 80: return launch_msd<ConstBase<80>, 66>(p, ConstBase<80>{}, num_cus, s);
-    default: return launch_msd<GenericBase, 390>(p, make_generic(p.base), num_cus, s);
+    case 40: return launch_msd(p, ConstBase<40>{}, num_cus, s);
+    case 50: return launch_msd(p, ConstBase<50>{}, num_cus, s);
+    case 80: return launch_msd(p, ConstBase<80>{}, num_cus, s);
+    default: return launch_msd(p, make_generic(p.base), num_cus, s);
     }
 }
 
