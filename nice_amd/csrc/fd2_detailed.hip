@@ -1,0 +1,687 @@
+// fd2_detailed.hip -- production finite-difference detailed kernel (gfx950).
+//
+// Computes exactly what process_range_detailed does (common/src/
+// client_process.rs:150-191: per n the unique-digit count of n^2 and n^3 in
+// base b, histogrammed, plus the near-miss list) for segments inside a base's
+// valid range, where n^2 and n^3 have fixed digit counts D2 + D3 = b.  It
+// replaces the reference's detailed_kernel (common/src/cuda/nice_kernels.cu:
+// 486-531); the design is MI355X-first, not a translation:
+//
+//  * Each lane walks a contiguous chunk n0 .. n0+len-1 (len <= B = b^2).
+//    n^2 and n^3 live in radix-B limbs (one limb = two base-b digits) and step
+//    by finite differences, never multiplying or dividing:
+//        S = n^2 += D1,  D1 = 2n + 1        += 2
+//        C = n^3 += E1,  E1 = 3n^2 + 3n + 1 += E2,  E2 = 6n + 6 += 6
+//  * Limb counts are template parameters picked by the host per segment
+//    (ND, NE, NE2 = limbs of D1, E1, E2 at the segment's end), so a step adds
+//    exactly the limbs that can change: S limbs [0, ND], C limbs [0, NE], E1
+//    limbs [0, NE2].  Carries out of those (probability ~1/B per step) and the
+//    limb-0 wraps of D1 / E2 take a rare, wave-uniform branch.
+//  * The per-step limbs are stored SCALED by the mask-table entry size ES and
+//    BIASED by 2^T - B: the stored word is directly the LDS byte address of the
+//    limb's digit-pair mask (no address arithmetic), and the radix-B carry is
+//    bit T + log2(ES) of the sum (one shift, one v_mad_i32_i24 to reduce).
+//  * n^2 mod B and n^3 mod B depend only on n mod B, so limb 0 of S and of C
+//    share ONE lookup in a low-digit table indexed by r = n0 mod B + i (< 2B:
+//    the table has 2B entries, so r never wraps inside a chunk).
+//  * Histogram: per-thread counters in LDS for a window of W unique counts
+//    around the distribution's bulk (b40: 17..32 holds all but 7e-5 of n); the
+//    rare counts outside the window (and every near-miss, which always lies
+//    above the window) take a divergent branch to a per-workgroup LDS
+//    histogram and the global near-miss list.  One flush per workgroup.
+//
+// The kernel is issue-bound on VALU and LDS together: b40 per n is 13 random
+// 8-byte LDS lookups (≈7 LDS cycles each per wave) and ≈105 VALU ops; see
+// DESIGN.md §3.1 for the cycle model and the measured roofline.
+#include <stdlib.h>
+
+#include <mutex>
+
+#include "host_math.hpp"
+#include "kernels.h"
+#include "nice_device.hpp"
+
+namespace nice {
+namespace fd2 {
+
+constexpr int log2ceil(unsigned v) { int t = 0; while ((1u << t) < v) t++; return t; }
+constexpr int ilog2(unsigned v) { int t = 0; while ((2u << t) <= v) t++; return t; }
+
+template <int BASE_, int ND_, int NE_, int NE2_, int PROBE_ = 0>
+struct Cfg {
+    static constexpr int BASE = BASE_;
+    // Bottleneck probes (timing experiments only, results are wrong): 1 = no
+    // table lookups (limb words OR-ed directly), 2 = no LDS histogram add.
+    static constexpr int PROBE = PROBE_;
+    static constexpr int ND = ND_, NE = NE_, NE2 = NE2_;
+    static constexpr int k = BASE / 5, r5 = BASE % 5;
+    // Digit counts inside the valid range (base_range.rs:14-32).
+    static constexpr int D2 = r5 == 0 ? 2 * k : (r5 == 4 ? 2 * k + 2 : 2 * k + 1);
+    static constexpr int D3 = r5 == 0 ? 3 * k : (r5 == 2 ? 3 * k + 1 : 3 * k + 2);
+    static constexpr int DN = r5 == 0 ? k : k + 1;
+    static constexpr int NS = cdiv(D2, 2), NC = cdiv(D3, 2), NX = cdiv(DN, 2);
+    static constexpr int SL = ND + 1, CL = NE + 1, EL = NE2 + 1;  // per-step limbs
+    static constexpr int S_TOPD = D2 - 2 * (NS - 1), C_TOPD = D3 - 2 * (NC - 1);
+    static constexpr u32 B = (u32)BASE * BASE;
+    static constexpr int T = log2ceil(B);
+    static constexpr u32 BT = (1u << T) - B;
+    static constexpr int MW = (BASE + 31) / 32;
+    static constexpr int ES = MW == 1 ? 4 : (MW == 2 ? 8 : 16);  // table entry bytes
+    static constexpr int SH = T + ilog2(ES);                     // carry bit of a scaled limb
+    static constexpr u32 ESB = ES * B, EBT = ES * BT;
+    static constexpr int WG = 512;
+    static constexpr int NBINS = BASE + 1;
+    // Histogram window [W0, W0 + W): per-thread counters (u32, or u16 halves
+    // shared by threads t and t + WG/2 when LDS is tight).
+    static constexpr int W = BASE == 40 ? 15 : (BASE == 50 ? 18 : 28);
+    static constexpr int W0 = BASE == 40 ? 18 : (BASE == 50 ? 21 : 33);
+    static constexpr bool HP = true;
+    static constexpr int HROW = HP ? WG / 2 : WG;  // counters per window row
+    static constexpr int HIST_BYTES = W * HROW * 4;
+    static constexpr int OUTL = HIST_BYTES;  // per-workgroup histogram of out-of-window counts
+    static constexpr int TB = (OUTL + 4 * NBINS + 15) / 16 * 16;  // digit-pair table
+    static constexpr bool LSD = MW <= 2;
+    static constexpr int TL = TB + (int)(B * ES);                // low-digit table (2B entries)
+    static constexpr int LDS_BYTES = TL + (LSD ? (int)(2 * B * ES) : 0);
+    static constexpr int LO = LSD ? 1 : 0;  // first stored / looked-up limb
+    // Low-digit entry, word 1: digit bits [0, DB), then flags and carries of
+    // the step n -> n+1, all functions of n mod B (limb 0 of S, C, D1, E1, E2
+    // is never stored): bit DB: D1 limb-0 wrap, DB+1: E2 limb-0 wrap; 4-bit
+    // fields at F0, F0+4, F0+8 hold 8 * (carry out of limb 0) of S += D1,
+    // C += E1, E1 += E2 (ES = 8, so a field IS the scaled carry).
+    static constexpr int DB = BASE - 32;
+    static constexpr u32 DMASK = (1u << (DB > 0 ? DB : 0)) - 1;
+    static constexpr u32 FLAGS = 3u << DB;
+    static constexpr int F0 = (DB + 2 + 3) / 4 * 4;
+    // LSD bases step C by C += 3S + N3 (N3 = 3n + 1, NN limbs): no E1 / E2
+    // state.  A C limb sum is < 5B, so its carry (0..4) is a multiply-high
+    // by MAGIC = ceil(2^32 / (ES B)) (exact over the range: static_assert).
+    static constexpr int NN = NX + 1;
+    static constexpr u32 DC = ES * B;
+    static constexpr u32 MAGIC = (u32)(((1ull << 32) + DC - 1) / DC);
+    static constexpr unsigned long long TMAX = (unsigned long long)ES * (5ull * B + 4);
+    static constexpr int FC = F0 + 4;  // 6-bit field: ES * (carry out of C limb 0)
+    // Waves per SIMD the LDS allows (the VGPR budget is set to match).
+    static constexpr int WPE0 = (163840 / LDS_BYTES) * (WG / 64) / 4;
+    static constexpr int WPE = WPE0 > 6 ? 6 : WPE0;
+    static_assert(SL < NS && CL < NC && EL <= NE, "FD layout needs cached high limbs");
+    static_assert(ND <= NX + 1 && NE2 <= NX + 1 && NE <= NS + 1, "difference limb counts");
+    static_assert(S_TOPD >= 1 && C_TOPD >= 1, "top limb");
+    static_assert(TB >= (int)EBT && TB - (int)EBT < 65536 && (!LSD || TL < 65536), "LDS offsets");
+    static_assert(LDS_BYTES <= 163840, "LDS");
+    static_assert(W0 + W <= NBINS, "window");
+    static_assert(!LSD || (ES == 8 && DB > 0 && FC + 6 <= 32), "low-digit entry layout");
+    static_assert(!LSD || ((unsigned long long)MAGIC * DC - (1ull << 32)) * TMAX < (1ull << 32),
+                  "C-limb carry magic");
+    static_assert(!LSD || (NN <= SL && NE >= NS), "C += 3S + N3 layout");
+};
+
+// v_mad_u32_u24 with an inline-constant multiplier (LLVM otherwise splits it
+// into v_mul_u32_u24 + v_add3_u32).
+template <u32 K>
+__device__ __forceinline__ u32 mad_u24(u32 a, u32 c) {
+    static_assert(K <= 64, "inline constant");
+    u32 r;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "n"(K), "v"(c));
+    return r;
+}
+
+template <class P>
+struct State {
+    u32 S[P::NS];    // n^2: limbs [0, SL) scaled+biased, [SL, NS) plain
+    u32 C[P::NC];    // n^3: same with CL
+    u32 D1[P::ND];   // scaled, plain
+    u32 E1[P::NE];   // scaled, plain
+    u32 E2[P::NE2];  // scaled, plain (non-LSD bases)
+    u32 N3[P::NN];   // LSD bases: 3n + 1, scaled, limb i < SL offset by -3 ES BT
+    u32 r8;          // low-digit table byte offset: ES * (n mod B + i)
+    u32 hi[P::MW];   // mask of the cached (rarely changing) limbs of S and C
+};
+
+template <class P>
+__device__ __forceinline__ void or_entry(const unsigned char *p, u32 (&m)[P::MW]) {
+    if constexpr (P::MW == 1) {
+        m[0] |= *(const u32 *)p;
+    } else if constexpr (P::MW == 2) {
+        uint2 v = *(const uint2 *)p;
+        m[0] |= v.x;
+        m[1] |= v.y;
+    } else {
+        uint4 v = *(const uint4 *)p;
+        m[0] |= v.x;
+        m[1] |= v.y;
+        m[2] |= v.z;
+    }
+}
+
+template <class P>
+__device__ __forceinline__ void or_plain(const unsigned char *smem, u32 v, int digits, u32 (&m)[P::MW]) {
+    if (digits == 2) {
+        or_entry<P>(smem + P::TB + v * P::ES, m);
+    } else {
+#pragma unroll
+        for (int w = 0; w < P::MW; w++) m[w] |= (v >> 5) == (u32)w ? 1u << (v & 31) : 0u;
+    }
+}
+
+template <class P>
+__device__ __forceinline__ void recompute_hi(State<P> &st, const unsigned char *smem) {
+#pragma unroll
+    for (int w = 0; w < P::MW; w++) st.hi[w] = 0;
+#pragma unroll
+    for (int i = P::SL; i < P::NS; i++) or_plain<P>(smem, st.S[i], i == P::NS - 1 ? P::S_TOPD : 2, st.hi);
+#pragma unroll
+    for (int i = P::CL; i < P::NC; i++) or_plain<P>(smem, st.C[i], i == P::NC - 1 ? P::C_TOPD : 2, st.hi);
+}
+
+// Radix-B normalisation of u64 column sums into M limbs (the value fits by the
+// host's choice of limb counts; a carry past limb M-1 is dropped).
+template <class P, int N, int M>
+__device__ __forceinline__ void normalize(const u64 (&acc)[N], u32 (&out)[M]) {
+    u64 cy = 0;
+#pragma unroll
+    for (int t = 0; t < M; t++) {
+        u64 v = (t < N ? acc[t] : 0) + cy;
+        out[t] = (u32)(v % P::B);
+        cy = v / P::B;
+    }
+}
+
+template <class P>
+__device__ __forceinline__ void init(State<P> &st, u64 n_lo, u64 n_hi, const unsigned char *smem) {
+    constexpr u32 B = P::B;
+    u32 w[4] = {(u32)n_lo, (u32)(n_lo >> 32), (u32)n_hi, (u32)(n_hi >> 32)};
+    u32 X[P::NX];
+#pragma unroll
+    for (int j = 0; j < P::NX; j++) {
+        u64 rem = 0;
+#pragma unroll
+        for (int q = 3; q >= 0; q--) {
+            u64 cur = (rem << 32) | w[q];
+            w[q] = (u32)(cur / B);
+            rem = cur % B;
+        }
+        X[j] = (u32)rem;
+    }
+    st.r8 = X[0] * P::ES;
+    {  // S = X^2
+        u64 acc[2 * P::NX];
+#pragma unroll
+        for (int t = 0; t < 2 * P::NX; t++) acc[t] = 0;
+#pragma unroll
+        for (int i = 0; i < P::NX; i++)
+#pragma unroll
+            for (int j = 0; j < P::NX; j++) acc[i + j] += (u64)X[i] * X[j];
+        normalize<P>(acc, st.S);
+    }
+    {  // C = S * X
+        u64 acc[P::NS + P::NX];
+#pragma unroll
+        for (int t = 0; t < P::NS + P::NX; t++) acc[t] = 0;
+#pragma unroll
+        for (int i = 0; i < P::NS; i++)
+#pragma unroll
+            for (int j = 0; j < P::NX; j++) acc[i + j] += (u64)st.S[i] * X[j];
+        normalize<P>(acc, st.C);
+    }
+    {  // D1 = 2n + 1
+        u64 acc[P::NX];
+#pragma unroll
+        for (int t = 0; t < P::NX; t++) acc[t] = 2ull * X[t] + (t == 0 ? 1 : 0);
+        normalize<P>(acc, st.D1);
+    }
+    {  // E1 = 3n^2 + 3n + 1
+        u64 acc[P::NS];
+#pragma unroll
+        for (int t = 0; t < P::NS; t++)
+            acc[t] = 3ull * st.S[t] + (t < P::NX ? 3ull * X[t] : 0) + (t == 0 ? 1 : 0);
+        normalize<P>(acc, st.E1);
+    }
+    {  // N3 = 3n + 1
+        u64 acc[P::NX];
+#pragma unroll
+        for (int t = 0; t < P::NX; t++) acc[t] = 3ull * X[t] + (t == 0 ? 1 : 0);
+        normalize<P>(acc, st.N3);
+    }
+    {  // E2 = 6n + 6
+        u64 acc[P::NX];
+#pragma unroll
+        for (int t = 0; t < P::NX; t++) acc[t] = 6ull * X[t] + (t == 0 ? 6 : 0);
+        normalize<P>(acc, st.E2);
+    }
+    recompute_hi<P>(st, smem);
+    if constexpr (P::LSD) st.S[0] = st.C[0] = st.D1[0] = st.N3[0] = 0;  // from the table
+#pragma unroll
+    for (int i = 0; i < P::SL; i++) st.S[i] = (st.S[i] + P::BT) * P::ES;
+#pragma unroll
+    for (int i = 0; i < P::CL; i++) st.C[i] = (st.C[i] + (P::LSD ? 0u : P::BT)) * P::ES;
+#pragma unroll
+    for (int i = 0; i < P::ND; i++) st.D1[i] *= P::ES;
+#pragma unroll
+    for (int i = 0; i < P::NE; i++) st.E1[i] *= P::ES;
+#pragma unroll
+    for (int i = 0; i < P::NE2; i++) st.E2[i] *= P::ES;
+#pragma unroll
+    for (int i = 0; i < P::NN; i++) st.N3[i] = st.N3[i] * P::ES - (i < P::SL ? 3 * P::EBT : 0u);
+}
+
+// +ES into scaled plain limbs [from, N) (rare path).
+template <class P, int N>
+__device__ __forceinline__ void carry_scaled(u32 (&x)[N], int from) {
+    u32 c = 1;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        if (i < from) continue;
+        u32 v = x[i] + c * P::ES;
+        c = v >= P::ESB;
+        x[i] = c ? 0u : v;
+    }
+}
+// +1 into plain limbs [from, N) (rare path).
+template <class P, int N>
+__device__ __forceinline__ void carry_plain(u32 (&x)[N], int from) {
+    u32 c = 1;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        if (i < from) continue;
+        u32 v = x[i] + c;
+        c = v == P::B;
+        x[i] = c ? 0u : v;
+    }
+}
+
+// +ES into N3 limbs [1, NN) (offset limbs, rare path).
+template <class P>
+__device__ __forceinline__ void carry_n3(State<P> &st) {
+    u32 c = 1;
+#pragma unroll
+    for (int i = 1; i < P::NN; i++) {
+        const u32 off = i < P::SL ? 3 * P::EBT : 0u;
+        u32 v = st.N3[i] + off + c * P::ES;
+        c = v >= P::ESB;
+        st.N3[i] = (c ? 0u : v) - off;
+    }
+}
+
+template <class P>
+__device__ __forceinline__ void rare(State<P> &st, const unsigned char *smem, u32 d1w, u32 e2w, u32 cS,
+                                     u32 cC, u32 cE) {
+    if (d1w) carry_scaled<P>(st.D1, 1);
+    if constexpr (P::LSD) {
+        if (e2w) carry_n3<P>(st);
+    } else {
+        if (e2w) carry_scaled<P>(st.E2, 1);
+        if (cE) carry_scaled<P>(st.E1, P::EL);
+    }
+    if (cS) carry_plain<P>(st.S, P::SL);
+    if (cC) carry_plain<P>(st.C, P::CL);
+    if (cS | cC) recompute_hi<P>(st, smem);
+}
+
+// One FD step n -> n+1.  w1 = word 1 of the low-digit entry of n (LSD bases):
+// limb 0 of every quantity lives in the table, so the chains start at limb 1
+// with the table's carries.  The carry leaves each limb as c8 = ES * carry,
+// (t >> T) & ES; the limb is reduced with one v_mad_i32_i24.
+template <class P>
+__device__ __forceinline__ void step(State<P> &st, const unsigned char *smem, u32 w1) {
+    constexpr u32 ES = P::ES;
+    if constexpr (P::LSD) {
+        // C += 3S + N3 (old S), limbs 1 .. CL-1; carry into limb 1 from the table.
+        u32 cC = __builtin_amdgcn_ubfe(w1, P::FC, 6);
+#pragma unroll
+        for (int i = 1; i < P::CL; i++) {
+            u32 t = st.C[i] + cC;
+            if (i < P::NN) t += st.N3[i];
+            else if (i < P::SL) t -= 3 * P::EBT;
+            // + 3S as one v_mad_u32_u24 (limbs < 2^24)
+            if (i < P::SL) t = mad_u24<3>(st.S[i], t);
+            else if (i < P::NS) t = mad_u24<3 * ES>(st.S[i], t);
+            const u32 c = __umulhi(t, P::MAGIC);
+            st.C[i] = t - c * P::DC;
+            cC = c * ES;
+        }
+        // S += D1, limbs 1 .. SL-1 (biased: carry = bit T of t >> LG).
+        u32 cS = __builtin_amdgcn_ubfe(w1, P::F0, 4);
+#pragma unroll
+        for (int i = 1; i < P::SL; i++) {
+            u32 t = st.S[i] + (i < P::ND ? st.D1[i] : 0u) + cS;
+            cS = (t >> P::T) & ES;
+            st.S[i] = t - cS * P::B;
+        }
+        st.r8 += ES;
+        if (((w1 & P::FLAGS) | cS | cC) != 0)
+            rare<P>(st, smem, w1 & (1u << P::DB), w1 & (2u << P::DB), cS, cC, 0);
+    } else {
+        u32 cS = 0, cC = 0, cE = 0;
+#pragma unroll
+        for (int i = 0; i < P::SL; i++) {
+            u32 t = st.S[i] + (i < P::ND ? st.D1[i] : 0u) + cS;
+            cS = (t >> P::T) & ES;
+            st.S[i] = t - cS * P::B;
+        }
+#pragma unroll
+        for (int i = 0; i < P::CL; i++) {
+            u32 t = st.C[i] + (i < P::NE ? st.E1[i] : 0u) + cC;
+            cC = (t >> P::T) & ES;
+            st.C[i] = t - cC * P::B;
+        }
+        // E1 += E2 (plain scaled: the bias is added for the carry test only).
+#pragma unroll
+        for (int i = 0; i < P::EL; i++) {
+            u32 t = st.E1[i] + (i < P::NE2 ? st.E2[i] : 0u) + cE;
+            cE = ((t + P::EBT) >> P::T) & ES;
+            st.E1[i] = t - cE * P::B;
+        }
+        st.r8 += ES;
+        st.D1[0] += 2 * ES;
+        st.E2[0] += 6 * ES;
+        const u32 d1w = st.D1[0] >= P::ESB, e2w = st.E2[0] >= P::ESB;
+        if ((cS | cC | cE | d1w | e2w) != 0) {
+            if (d1w) st.D1[0] -= P::ESB;
+            if (e2w) st.E2[0] -= P::ESB;
+            rare<P>(st, smem, d1w, e2w, cS, cC, cE);
+        }
+    }
+}
+
+template <class P>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P::WPE, P::WPE)))
+fd2_kernel(u64 start_lo, u64 start_hi, u32 nunits, u32 chunk, u32 cutoff,
+           u64 *__restrict__ hist_out, NumOut out) {
+    // Static LDS: its address is a compile-time constant, so a lookup is one
+    // ds_read with the table offset in the instruction's immediate field.
+    __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDS_BYTES];
+    u32 *hist = (u32 *)smem;
+    u32 *outl = (u32 *)(smem + P::OUTL);
+    const u32 tid = threadIdx.x;
+
+    // Digit-pair table: entry e = d1*b + d0 marks d0 and d1.  Low-digit table:
+    // entry r (< 2B) marks the two low digits of r^2 and of r^3 (mod B).
+    for (u32 e = tid; e < P::B; e += P::WG) {
+        u32 v[4] = {0, 0, 0, 0};
+        auto mark = [&](u32 x) {
+            u32 d0 = x % P::BASE, d1 = x / P::BASE;
+            v[d0 >> 5] |= 1u << (d0 & 31);
+            v[d1 >> 5] |= 1u << (d1 & 31);
+        };
+        auto put = [&](unsigned char *p) {
+            if constexpr (P::ES == 4) *(u32 *)p = v[0];
+            else if constexpr (P::ES == 8) *(uint2 *)p = make_uint2(v[0], v[1]);
+            else *(uint4 *)p = make_uint4(v[0], v[1], v[2], v[3]);
+        };
+        mark(e);
+        put(smem + P::TB + e * P::ES);
+        if constexpr (P::LSD) {
+            v[0] = v[1] = v[2] = v[3] = 0;
+            const u32 B = P::B;
+            const u32 s0 = (u32)((u64)e * e % B), c0 = (u32)((u64)s0 * e % B);
+            mark(s0);
+            mark(c0);
+            const u32 d1 = (2 * e + 1) % B, n3 = (3 * e + 1) % B;
+            v[1] |= (d1 + 2 >= B ? 1u : 0u) << P::DB;                // D1 limb-0 wrap
+            v[1] |= (n3 + 3 >= B ? 2u : 0u) << P::DB;                // N3 limb-0 wrap
+            v[1] |= (s0 + d1 >= B ? 8u : 0u) << P::F0;               // S  += D1 carry
+            v[1] |= (P::ES * ((c0 + 3 * s0 + n3) / B)) << P::FC;      // C += 3S + N3 carry
+            put(smem + P::TL + e * P::ES);
+            put(smem + P::TL + (e + P::B) * P::ES);
+        }
+    }
+    for (u32 i = tid; i < (u32)(P::TB / 4); i += P::WG) hist[i] = 0;
+    __syncthreads();
+
+    // Window counters: row u - W0, column tid (u32) or tid mod WG/2 (u16 half).
+    const u32 hbase = (P::HP ? tid % P::HROW : tid) * 4;
+    const u32 hinc = P::HP && tid >= (u32)P::HROW ? 0x10000u : 1u;
+    const u32 stride = gridDim.x * P::WG;
+    u32 probe_acc = 0;
+    for (u32 unit = blockIdx.x * P::WG + tid; unit < nunits; unit += stride) {
+        u64 n0_lo = start_lo, n0_hi = start_hi;
+        add_u128(n0_lo, n0_hi, (u64)unit * chunk);
+        State<P> st;
+        init<P>(st, n0_lo, n0_hi, smem);
+        const u32 r80 = st.r8;
+        for (u32 i = 0; i < chunk; i++) {
+            u32 m[P::MW], w1 = 0;
+#pragma unroll
+            for (int w = 0; w < P::MW; w++) m[w] = st.hi[w];
+            if constexpr (P::PROBE & 1) {
+                m[0] |= st.r8;
+                w1 = st.r8 & 0xff;
+#pragma unroll
+                for (int q = P::LO; q < P::SL; q++) m[q & 1] |= st.S[q];
+#pragma unroll
+                for (int q = P::LO; q < P::CL; q++) m[q & 1] |= st.C[q];
+            } else {
+                if constexpr (P::LSD) {
+                    const uint2 v = *(const uint2 *)(smem + P::TL + st.r8);
+                    m[0] |= v.x;
+                    m[1] |= v.y & P::DMASK;
+                    w1 = v.y;
+                }
+#pragma unroll
+                for (int q = P::LO; q < P::SL; q++) or_entry<P>(smem + (P::TB - P::EBT) + st.S[q], m);
+#pragma unroll
+                for (int q = P::LO; q < P::CL; q++)
+                    or_entry<P>(smem + (P::LSD ? P::TB : P::TB - P::EBT) + st.C[q], m);
+            }
+            u32 uw = (u32)(-P::W0);
+#pragma unroll
+            for (int w = 0; w < P::MW; w++) uw += __popc(m[w]);
+            if (uw < (u32)P::W) {
+                if constexpr (P::PROBE & 2) probe_acc++;
+                else atomicAdd((u32 *)(smem + uw * (P::HROW * 4) + hbase), hinc);
+            } else {
+                const u32 u = uw + P::W0;
+                atomicAdd(&outl[u], 1u);
+                if (u > cutoff) {
+                    u64 lo = n0_lo, hi = n0_hi;
+                    add_u128(lo, hi, (st.r8 - r80) / P::ES);  // = i (keeps i scalar)
+                    u32 pos = atomicAdd(out.count, 1u);
+                    if (pos < out.cap) {
+                        out.n[2 * (u64)pos] = lo;
+                        out.n[2 * (u64)pos + 1] = hi;
+                        out.u[pos] = u;
+                    }
+                }
+            }
+            step<P>(st, smem, w1);
+        }
+    }
+    if constexpr ((P::PROBE & 2) != 0) atomicAdd(&outl[P::W0], probe_acc);  // mass only
+    __syncthreads();
+    const u32 lane = tid & 63, wave = tid >> 6;
+    for (u32 row = wave; row < (u32)P::W; row += P::WG / 64) {
+        u32 s = 0;
+#pragma unroll
+        for (int q = 0; q < P::HROW / 64; q++) {
+            const u32 v = hist[row * P::HROW + lane + 64 * q];
+            s += P::HP ? (v & 0xffffu) + (v >> 16) : v;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+        if (lane == 0 && s) atomicAdd((unsigned long long *)&hist_out[P::W0 + row], (unsigned long long)s);
+    }
+    if (tid < (u32)P::NBINS && outl[tid])
+        atomicAdd((unsigned long long *)&hist_out[tid], (unsigned long long)outl[tid]);
+}
+
+template <class P>
+static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s) {
+    auto kern = fd2_kernel<P>;
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)kern, P::WG, 0);
+    if (e != hipSuccess) return e;
+    if (per_cu < 1) per_cu = 1;
+    const u64 lanes = (u64)num_cus * per_cu * P::WG;
+    // u16 counters: at most 65535 numbers per lane per launch.
+    const u64 max_count = P::HP ? lanes * 60000ull : ~0ull;
+    // Every near-miss count must lie above the window (it is recorded on the
+    // out-of-window branch).
+    if (p.cutoff + 1 < (u32)(P::W0 + P::W)) return hipErrorInvalidValue;
+    DetailedLaunch q = p;
+    u64 left = p.count;
+    while (left) {
+        const u64 cnt = left < max_count ? left : max_count;
+        // Chunks of <= B numbers (low-digit table), about 3 per lane.
+        const u64 per_lane = (cnt + lanes - 1) / lanes;
+        const u64 units_per_lane = (per_lane + P::B - 1) / P::B < 3 ? 3 : (per_lane + P::B - 1) / P::B;
+        u64 chunk = (cnt + lanes * units_per_lane - 1) / (lanes * units_per_lane);
+        if (chunk < 1) chunk = 1;
+        if (chunk > P::B) chunk = P::B;
+        // Odd chunks: lane l of a wave then sits at n mod B = r0 + chunk * l,
+        // so its low-digit entries fall on 32 distinct bank pairs per half-wave
+        // (B is a multiple of 32 for the LSD bases): conflict-free lookups.
+        if (P::LSD && chunk > 1 && chunk % 2 == 0) chunk--;
+        u64 nunits = cnt / chunk;
+        if (nunits > 0xffffffffull) return hipErrorInvalidValue;
+        if (nunits) {
+            u64 grid = (nunits + P::WG - 1) / P::WG;
+            const u64 max_grid = (u64)num_cus * per_cu;
+            if (grid > max_grid) grid = max_grid;
+            hipLaunchKernelGGL(kern, dim3((u32)grid), dim3(P::WG), 0, s, q.start_lo,
+                               q.start_hi, (u32)nunits, (u32)chunk, q.cutoff, q.hist, q.out);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        const u64 tail = cnt - nunits * chunk;  // < chunk: one unit of its own
+        if (tail) {
+            u64 lo = q.start_lo, hi = q.start_hi;
+            add_u128(lo, hi, nunits * chunk);
+            hipLaunchKernelGGL(kern, dim3(1), dim3(P::WG), 0, s, lo, hi, 1u, (u32)tail,
+                               q.cutoff, q.hist, q.out);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        add_u128(q.start_lo, q.start_hi, cnt);
+        left -= cnt;
+    }
+    return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------
+// Host: limb counts per segment.  For a segment [a, e) the last FD state a
+// lane builds is for n = e (one step past its last number), so D1(e) = 2e+1,
+// E1(e) = 3e^2+3e+1 and E2(e) = 6e+6 must fit ND, NE, NE2 radix-b^2 limbs.
+// ---------------------------------------------------------------------------
+struct Combo {
+    int nd, ne, ne2;
+};
+
+static int limbs_of(const Nat &x, const std::vector<Nat> &pw) {
+    int k = 0;
+    while (k < (int)pw.size() && x.cmp(pw[k]) >= 0) k++;
+    return k;  // smallest k with x < B^k
+}
+
+static Combo combo_at(uint32_t base, u128 e, const std::vector<Nat> &pw) {
+    Nat n = Nat::from(e);
+    Nat d1 = n;
+    d1.mul_small(2);
+    Nat one = Nat::from(1);
+    auto add = [](Nat a, const Nat &b) {
+        a.l.resize(std::max(a.l.size(), b.l.size()) + 1, 0);
+        uint64_t c = 0;
+        for (size_t i = 0; i < a.l.size(); i++) {
+            uint64_t t = (uint64_t)a.l[i] + (i < b.l.size() ? b.l[i] : 0) + c;
+            a.l[i] = (uint32_t)t;
+            c = t >> 32;
+        }
+        a.trim();
+        return a;
+    };
+    d1 = add(d1, one);
+    Nat n3 = n;
+    n3.mul_small(3);
+    Nat e1 = add(add(n3.mul(n), n3), one);  // 3n^2 + 3n + 1
+    Nat e2 = n;
+    e2.mul_small(6);
+    e2 = add(e2, Nat::from(6));
+    (void)base;
+    return Combo{limbs_of(d1, pw), limbs_of(e1, pw), limbs_of(e2, pw)};
+}
+
+struct BaseThresholds {
+    std::vector<Nat> pw;     // B^k
+    std::vector<u128> cuts;  // n where the combo changes, ascending, inside the range
+};
+
+static const BaseThresholds &thresholds(uint32_t base) {
+    static std::mutex mu;
+    static BaseThresholds cache[129];
+    static bool have[129] = {};
+    std::lock_guard<std::mutex> g(mu);
+    BaseThresholds &t = cache[base];
+    if (have[base]) return t;
+    const uint32_t B = base * base;
+    for (int k = 0; k < 40; k++) t.pw.push_back(Nat::pow(B, k));
+    u128 rs = 0, re = 0;
+    base_range(base, rs, re);
+    // Walk the range: binary-search each change of combo_at.
+    u128 a = rs;
+    Combo cur = combo_at(base, a + 1, t.pw);
+    while (true) {
+        Combo last = combo_at(base, re, t.pw);
+        if (last.nd == cur.nd && last.ne == cur.ne && last.ne2 == cur.ne2) break;
+        u128 lo = a + 1, hi = re;  // smallest e in (a, re] whose combo differs
+        while (lo < hi) {
+            u128 mid = lo + (hi - lo) / 2;
+            Combo c = combo_at(base, mid, t.pw);
+            if (c.nd == cur.nd && c.ne == cur.ne && c.ne2 == cur.ne2) lo = mid + 1;
+            else hi = mid;
+        }
+        // Segments ending at e <= lo - 1 use `cur`; the cut is at n = lo - 1
+        // (a segment [x, lo-1) ends at e = lo - 1).
+        t.cuts.push_back(lo - 1);
+        a = lo - 1;
+        cur = combo_at(base, lo, t.pw);
+    }
+    have[base] = true;
+    return t;
+}
+
+#define FD2_COMBOS(X)                                                                           \
+    X(40, 4, 8, 5) X(40, 5, 8, 5) X(40, 5, 9, 5) X(50, 5, 10, 6) X(50, 6, 10, 6) X(50, 6, 11, 6) \
+        X(80, 8, 16, 9) X(80, 9, 16, 9) X(80, 9, 17, 9)
+
+static hipError_t launch_segment(const DetailedLaunch &p, int num_cus, hipStream_t s) {
+    const BaseThresholds &t = thresholds(p.base);
+    u128 a = ((u128)p.start_hi << 64) | p.start_lo;
+    const Combo c = combo_at(p.base, a + p.count, t.pw);
+    const int probe = getenv("NICE_FD2_PROBE") ? atoi(getenv("NICE_FD2_PROBE")) : 0;
+    if (probe && p.base == 40 && c.nd == 4 && c.ne == 8 && c.ne2 == 5) {
+        if (probe == 1) return launch_cfg<Cfg<40, 4, 8, 5, 1>>(p, num_cus, s);
+        if (probe == 2) return launch_cfg<Cfg<40, 4, 8, 5, 2>>(p, num_cus, s);
+        if (probe == 3) return launch_cfg<Cfg<40, 4, 8, 5, 3>>(p, num_cus, s);
+    }
+#define X(B_, ND_, NE_, NE2_)                                              \
+    if (p.base == B_ && c.nd == ND_ && c.ne == NE_ && c.ne2 == NE2_)        \
+        return launch_cfg<Cfg<B_, ND_, NE_, NE2_>>(p, num_cus, s);
+    FD2_COMBOS(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
+}  // namespace fd2
+
+bool fd2_supported(uint32_t base) { return base == 40 || base == 50 || base == 80; }
+
+// In-range segment [start, start + count): split at the limb-count cuts, one
+// launch (plus a tail launch) per piece.
+hipError_t launch_detailed_fd2(const DetailedLaunch &p, int num_cus, hipStream_t s) {
+    if (!fd2_supported(p.base)) return hipErrorInvalidValue;
+    const fd2::BaseThresholds &t = fd2::thresholds(p.base);
+    u128 a = ((u128)p.start_hi << 64) | p.start_lo;
+    const u128 e = a + p.count;
+    DetailedLaunch q = p;
+    for (size_t i = 0; i <= t.cuts.size() && a < e; i++) {
+        u128 stop = i < t.cuts.size() && t.cuts[i] < e ? t.cuts[i] : e;
+        if (stop <= a) continue;
+        q.start_lo = (uint64_t)a;
+        q.start_hi = (uint64_t)(a >> 64);
+        q.count = (uint64_t)(stop - a);
+        hipError_t err = fd2::launch_segment(q, num_cus, s);
+        if (err != hipSuccess) return err;
+        a = stop;
+    }
+    return hipSuccess;
+}
+
+}  // namespace nice

@@ -29,6 +29,9 @@ struct DetailedLaunch {
 bool fd_supported(uint32_t base);
 // Launch the FD kernel over an in-range segment.  grid_cap: max workgroups.
 hipError_t launch_detailed_fd(const DetailedLaunch &p, int num_cus, hipStream_t s, int variant = 0);
+// Production FD kernel (fd2_detailed.hip): bases 40, 50, 80, in-range segments.
+bool fd2_supported(uint32_t base);
+hipError_t launch_detailed_fd2(const DetailedLaunch &p, int num_cus, hipStream_t s);
 // Generic per-n kernel: any base 2..128, any n < 2^128.
 hipError_t launch_detailed_generic(const DetailedLaunch &p, int num_cus, hipStream_t s);
 

@@ -249,8 +249,11 @@ int enqueue_detailed(Device &d, u128 s, u128 e, uint32_t base, bool &used_fd, ui
             p.start_lo = lo64(a);
             p.start_hi = hi64(a);
             p.count = c;
-            hipError_t err = fd ? nice::launch_detailed_fd(p, d.num_cus, d.stream, fd_variant())
-                                : nice::launch_detailed_generic(p, d.num_cus, d.stream);
+            const int var = fd_variant();
+            hipError_t err = !fd ? nice::launch_detailed_generic(p, d.num_cus, d.stream)
+                             : var == 0 && nice::fd2_supported(base)
+                                 ? nice::launch_detailed_fd2(p, d.num_cus, d.stream)
+                                 : nice::launch_detailed_fd(p, d.num_cus, d.stream, var);
             if (err != hipSuccess)
                 return fail(NICE_ERR_HIP, std::string("detailed launch: ") + hipGetErrorString(err));
             if (fd) {

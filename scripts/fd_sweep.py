@@ -10,7 +10,7 @@ sys.path.insert(0, ROOT)
 import nice_amd as N  # noqa: E402
 
 cfg = [(40, 10 ** 9), (50, 10 ** 9), (80, 2 * 10 ** 8)]
-variants = [1, 2, 3, 8, 9, 10, 11]
+variants = [int(v) for v in os.environ.get("SWEEP_VARIANTS", "0,1,2,3,8,9,10,11").split(",")]
 reps = 3
 ctx = N.GpuContext(0)
 res = {}

@@ -79,6 +79,66 @@ def test_fd_kernel_segments(ctx, base):
         check_detailed(ctx, mid + 7, mid + 7 + size, base)
 
 
+def _fd2_cuts(base):
+    """n where the production FD kernel's limb counts (D1 = 2e+1, E1 =
+    3e^2+3e+1, E2 = 6e+6 in radix b^2 at a segment end e) change inside the
+    valid range -- the host splits launches there (fd2_detailed.hip)."""
+    B = base * base
+
+    def limbs(x):
+        k = 0
+        while x >= B ** k:
+            k += 1
+        return k
+
+    def combo(e):
+        return (limbs(2 * e + 1), limbs(3 * e * e + 3 * e + 1), limbs(6 * e + 6))
+
+    s, e = O.base_range(base)
+    cuts, a = [], s
+    while combo(a + 1) != combo(e):
+        lo, hi, cur = a + 1, e, combo(a + 1)
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if combo(mid) == cur:
+                lo = mid + 1
+            else:
+                hi = mid
+        cuts.append(lo - 1)
+        a = lo - 1
+    return cuts
+
+
+@pytest.mark.parametrize("base", [40, 50, 80])
+def test_fd_kernel_limb_count_cuts(ctx, base):
+    """Segments ending on, just past and straddling each limb-count cut use
+    neighbouring kernel instantiations; all must agree with the oracle."""
+    cuts = _fd2_cuts(base)
+    assert len(cuts) == 2
+    for c in cuts:
+        check_detailed(ctx, c - 200_000, c + 200_000, base)
+        check_detailed(ctx, c - 70_001, c, base)
+        check_detailed(ctx, c, c + 70_001, base)
+        check_detailed(ctx, c - 1, c + 2, base)
+
+
+def test_fd_kernel_generations_agree(ctx):
+    """The production FD kernel and the first-generation FD kernel
+    (NICE_FD_VARIANT=1) give identical results on large in-range fields."""
+    import os
+    for base, size in ((40, 3 * 10 ** 8), (50, 10 ** 8), (80, 5 * 10 ** 7)):
+        s, e = O.base_range(base)
+        a = s + (e - s) // 2
+        want = ctx.detailed_raw(a, a + size, base)
+        os.environ["NICE_FD_VARIANT"] = "1"
+        try:
+            got = ctx.detailed_raw(a, a + size, base)
+        finally:
+            os.environ["NICE_FD_VARIANT"] = "0"
+        assert got == want, base
+        assert sum(want[0]) == size
+
+
 def test_fd_kernel_random_windows(ctx):
     rng = random.Random(7)
     for base in (40, 50, 80):
