@@ -50,6 +50,17 @@ def parse():
     return p.parse_args()
 
 
+def pmc_traffic():
+    """HBM bytes per main launch of the detailed kernel, from the committed PMC
+    pass (scripts/gpu_pmc.sh -> profiles/r01/traffic.json); None if absent."""
+    p = os.path.join(ROOT, "profiles", "r01", "traffic.json")
+    try:
+        with open(p) as f:
+            return json.load(f)["bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def rank_field(base_start: int, rank: int):
     """Weak scaling: rank r owns the r-th consecutive 1e9 field of base 40."""
     start = base_start + rank * FIELD_SIZE
@@ -216,13 +227,15 @@ def main():
         line["detailed_numbers_per_sec"] = FIELD_SIZE / (sum(det_ms) / len(det_ms) / 1e3)
         line["detailed_ms"] = sum(det_ms) / len(det_ms)
         line["roofline"] = {
-            "bound": "valu", "kernel": "detailed_fd_kernel<40>",
+            "bound": "valu", "kernel": "nice::fd2::fd2_kernel<Cfg<40, 4, 8, 5>>",
             "achieved": achieved, "peak": PEAK_INT32_TOPS, "unit": "int32 Tops/s",
-            "frac": achieved / PEAK_INT32_TOPS, "traffic": None,
+            "frac": achieved / PEAK_INT32_TOPS, "traffic": pmc_traffic(),
             "kernel_ms": kms,
             "work_per_unit": f"{W_ALG} int32 ops per n (4 per digit x {BASE} digits, SURVEY 8d)",
-            "note": "integer-VALU bound (no HBM stream, no contraction); kernel time from HIP "
-                    "events on the launch stream; traffic: no input stream (outputs < 1 KB)",
+            "note": "integer-VALU/LDS bound (no HBM stream, no contraction); kernel time from "
+                    "HIP events on the launch stream (main + tail launch of one field); traffic: "
+                    "HBM bytes per launch from the committed PMC pass (profiles/r01/traffic.json, "
+                    "FETCH_SIZE x2 + WRITE_SIZE), the field's bounds are the only input",
         }
     if nice_ms:
         line["niceonly_numbers_per_sec"] = FIELD_SIZE / (sum(nice_ms) / len(nice_ms) / 1e3)

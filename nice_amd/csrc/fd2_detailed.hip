@@ -385,9 +385,8 @@ __device__ __forceinline__ void step(State<P> &st, const unsigned char *smem, u3
 }
 
 template <class P>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P::WPE, P::WPE)))
-fd2_kernel(u64 start_lo, u64 start_hi, u32 nunits, u32 chunk, u32 cutoff,
-           u64 *__restrict__ hist_out, NumOut out) {
+__device__ __forceinline__ void fd2_body(u64 start_lo, u64 start_hi, u32 nunits, u32 chunk, u32 cutoff,
+                                         u64 *__restrict__ hist_out, NumOut out) {
     // Static LDS: its address is a compile-time constant, so a lookup is one
     // ds_read with the table offset in the instruction's immediate field.
     __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDS_BYTES];
@@ -505,6 +504,21 @@ fd2_kernel(u64 start_lo, u64 start_hi, u32 nunits, u32 chunk, u32 cutoff,
         atomicAdd((unsigned long long *)&hist_out[tid], (unsigned long long)outl[tid]);
 }
 
+// Main launch: units of `chunk` numbers.  Tail launch: the < chunk numbers
+// left over, one per lane (its own symbol, so profiles show it apart).
+template <class P>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P::WPE, P::WPE)))
+fd2_kernel(u64 start_lo, u64 start_hi, u32 nunits, u32 chunk, u32 cutoff, u64 *__restrict__ hist_out,
+           NumOut out) {
+    fd2_body<P>(start_lo, start_hi, nunits, chunk, cutoff, hist_out, out);
+}
+template <class P>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P::WPE, P::WPE)))
+fd2_tail_kernel(u64 start_lo, u64 start_hi, u32 nunits, u32 cutoff, u64 *__restrict__ hist_out,
+                NumOut out) {
+    fd2_body<P>(start_lo, start_hi, nunits, 1u, cutoff, hist_out, out);
+}
+
 template <class P>
 static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s) {
     auto kern = fd2_kernel<P>;
@@ -542,12 +556,12 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
                                q.start_hi, (u32)nunits, (u32)chunk, q.cutoff, q.hist, q.out);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
-        const u64 tail = cnt - nunits * chunk;  // < chunk: one unit of its own
+        const u64 tail = cnt - nunits * chunk;  // < chunk <= B: one number per lane
         if (tail) {
             u64 lo = q.start_lo, hi = q.start_hi;
             add_u128(lo, hi, nunits * chunk);
-            hipLaunchKernelGGL(kern, dim3(1), dim3(P::WG), 0, s, lo, hi, 1u, (u32)tail,
-                               q.cutoff, q.hist, q.out);
+            hipLaunchKernelGGL(fd2_tail_kernel<P>, dim3((u32)((tail + P::WG - 1) / P::WG)), dim3(P::WG), 0,
+                               s, lo, hi, (u32)tail, q.cutoff, q.hist, q.out);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
         add_u128(q.start_lo, q.start_hi, cnt);
