@@ -52,6 +52,7 @@ struct NiceonlyLaunch {
     const uint32_t *residues;      // R valid residues mod M, ascending
     uint32_t R, M;
     uint32_t base;
+    uint32_t in_range;             // every candidate inside the base's valid range
     NumOut out;
 };
 bool niceonly_specialised(uint32_t base);
@@ -78,8 +79,10 @@ struct MsdLaunch {
     Leaf *leaves;
     uint32_t leaf_cap;
     const uint32_t *residues;
+    const uint32_t *ranks;        // ranks[r] = lower_bound(residues, r), r in [0, M]
     uint32_t R, M;
     uint32_t base;
+    uint32_t in_range;            // the batch lies inside the base's valid range
 };
 // Enqueue the init + 22 level kernels (no host sync).
 hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s);

@@ -81,7 +81,8 @@ struct Device {
     uint32_t list_cap = 0;
     uint64_t *h_hist = nullptr;   // pinned
     uint32_t *h_count = nullptr;  // pinned
-    std::map<uint32_t, uint32_t *> residues;  // base -> device residue table
+    std::map<uint32_t, uint32_t *> residues;  // base*8+k -> device residue table
+    std::map<uint32_t, uint32_t *> ranks;     // base*8+k -> lower_bound(residues, r), r in [0, M]
     LeafBuf desc[2];
     int desc_next = 0;
     MsdBuf msd;
@@ -182,6 +183,7 @@ void device_free(Device &d) {
     (void)hipSetDevice(d.id);
     (void)hipStreamSynchronize(d.stream);
     for (auto &kv : d.residues) (void)hipFree(kv.second);
+    for (auto &kv : d.ranks) (void)hipFree(kv.second);
     for (auto &b : d.desc) {
         if (b.h) {
             (void)hipHostFree(b.h);
@@ -518,6 +520,10 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
         return NICE_OK;
     }
     auto table = g_stride.get(base, k);
+    // Whole field inside the base's valid range: the kernels take their
+    // fixed-digit-count fast paths (radix_fast.hpp).
+    u128 vr_s = 0, vr_e = 0;
+    const uint32_t in_range = nice::base_range(base, vr_s, vr_e) == 1 && vr_s <= s && e <= vr_e ? 1u : 0u;
     const uint32_t R = (uint32_t)table->residues.size();
     const uint64_t M = table->modulus;
     if (M > 0xffffffffull) return fail(NICE_ERR_INVALID, "stride modulus exceeds u32");
@@ -528,6 +534,17 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
             HIPCHK(hipMalloc(&p, (size_t)R * 4));
             HIPCHK(hipMemcpy(p, table->residues.data(), (size_t)R * 4, hipMemcpyHostToDevice));
             d.residues[base * 8 + k] = p;
+            // rank[r] = lower_bound(residues, r): the device MSD turns a leaf's
+            // end points into stride indices with one load each.
+            std::vector<uint32_t> rank((size_t)M + 1);
+            uint32_t g = 0;
+            for (uint64_t r = 0; r <= M; r++) {
+                while (g < R && table->residues[g] < r) g++;
+                rank[r] = g;
+            }
+            HIPCHK(hipMalloc(&p, rank.size() * 4));
+            HIPCHK(hipMemcpy(p, rank.data(), rank.size() * 4, hipMemcpyHostToDevice));
+            d.ranks[base * 8 + k] = p;
         }
         HIPCHK(hipMemsetAsync(d.d_count + 1, 0, 4, d.stream));
         int rc = ensure_list(d, kNiceCap);
@@ -575,9 +592,11 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
             mp.leaves = d.msd.leaves;
             mp.leaf_cap = d.msd.leaf_cap;
             mp.residues = d.residues[base * 8 + k];
+            mp.ranks = d.ranks[base * 8 + k];
             mp.R = R;
             mp.M = (uint32_t)M;
             mp.base = base;
+            mp.in_range = in_range;
             hipError_t err = nice::launch_msd_device(mp, d.num_cus, d.stream);
             if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("msd launch: ") + hipGetErrorString(err));
             nice::NiceonlyLaunch p{};
@@ -588,6 +607,7 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
             p.R = R;
             p.M = (uint32_t)M;
             p.base = base;
+            p.in_range = in_range;
             p.out = nice::NumOut{d.d_list_n, nullptr, d.d_count + 1, d.list_cap};
             err = nice::launch_niceonly(p, d.num_cus, d.stream);
             if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("niceonly launch: ") + hipGetErrorString(err));
@@ -701,6 +721,7 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
             p.R = R;
             p.M = (uint32_t)M;
             p.base = base;
+            p.in_range = in_range;
             p.out = nice::NumOut{d.d_list_n, nullptr, d.d_count + 1, d.list_cap};
             hipError_t err = nice::launch_niceonly(p, d.num_cus, d.stream);
             if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("niceonly launch: ") + hipGetErrorString(err));

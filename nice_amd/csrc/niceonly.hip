@@ -20,9 +20,20 @@
 // recursion is depth-limited (22), so 23 launches per batch, no host sync.
 #include "kernels.h"
 #include "nice_device.hpp"
+#include "radix_fast.hpp"
 
 namespace nice {
 
+template <class G>
+struct IsConst {
+    static constexpr bool value = false;
+    static constexpr int base = 0;
+};
+template <int B>
+struct IsConst<ConstBase<B>> {
+    static constexpr bool value = true;
+    static constexpr int base = B;
+};
 
 // ---------------------------------------------------------------------------
 // Candidate check kernel
@@ -65,7 +76,13 @@ niceonly_kernel(NiceonlyLaunch p, G g) {
                 const u32 idx = gi - cyc * p.R;
                 u64 n_lo = b0lo, n_hi = b0hi;
                 add_u128(n_lo, n_hi, (u64)cyc * p.M + p.residues[idx]);
-                if (is_nice_dev(n_lo, n_hi, g)) {
+                bool nice;
+                if constexpr (IsConst<G>::value) {
+                    nice = p.in_range ? is_nice_fast<IsConst<G>::base>(n_lo, n_hi) : is_nice_dev(n_lo, n_hi, g);
+                } else {
+                    nice = is_nice_dev(n_lo, n_hi, g);
+                }
+                if (nice) {
                     u32 pos = atomicAdd(p.out.count, 1u);
                     if (pos < p.out.cap) {
                         p.out.n[2 * (u64)pos] = n_lo;
@@ -202,16 +219,7 @@ __device__ void emit_leaf(u64 a_lo, u64 a_hi, u64 size, const MsdLaunch &p) {
     add_u128(e_lo, e_hi, size);
     u64 qe_lo = e_lo, qe_hi = e_hi;
     const u32 re = divmod_u128(qe_lo, qe_hi, p.M);
-    auto lower_bound = [&](u32 x) {
-        u32 lo = 0, hi = p.R;
-        while (lo < hi) {
-            u32 mid = (lo + hi) >> 1;
-            if (p.residues[mid] < x) lo = mid + 1;
-            else hi = mid;
-        }
-        return lo;
-    };
-    const u32 g0 = lower_bound(ra), g1 = lower_bound(re);
+    const u32 g0 = p.ranks[ra], g1 = p.ranks[re];
     // cycles between the two ends (< 2^64 / M for any batch)
     const u64 dcyc = qe_lo - q_lo;
     const u64 count = dcyc * p.R + g1 - g0;
@@ -255,7 +263,16 @@ msd_level_kernel(MsdLaunch p, u32 level, G g) {
         if (!leaf) {
             u64 l_lo = nd.lo, l_hi = nd.hi;
             add_u128(l_lo, l_hi, nd.size - 1);
-            if (nd.size != 1 && msd_skippable<G>(nd.lo, nd.hi, l_lo, l_hi, g)) continue;
+            bool skip = false;
+            if (nd.size != 1) {
+                if constexpr (IsConst<G>::value) {
+                    skip = p.in_range ? msd_skippable_fast<IsConst<G>::base>(nd.lo, nd.hi, l_lo, l_hi)
+                                      : msd_skippable<G>(nd.lo, nd.hi, l_lo, l_hi, g);
+                } else {
+                    skip = msd_skippable<G>(nd.lo, nd.hi, l_lo, l_hi, g);
+                }
+            }
+            if (skip) continue;
             leaf = nd.size < 2 * p.floor_size;
         }
         if (leaf) {
@@ -313,9 +330,22 @@ hipError_t launch_niceonly(const NiceonlyLaunch &p, int num_cus, hipStream_t s) 
 template <class G>
 static hipError_t launch_msd(const MsdLaunch &p, const G &g, int num_cus, hipStream_t s) {
     hipLaunchKernelGGL(msd_init_kernel, dim3(256), dim3(256), 0, s, p);
-    const u32 grid = (u32)num_cus * 8;
-    for (u32 level = 0; level <= 22; level++)
-        hipLaunchKernelGGL((msd_level_kernel<G>), dim3(grid), dim3(256), 0, s, p, level, g);
+    const u64 nchunks = (p.batch_size + p.chunk - 1) / p.chunk;
+    // A node of level d has at most ceil(chunk / 2^d) numbers and splits only
+    // if it holds >= 2 * floor, so levels past the first d with
+    // ceil(chunk / 2^d) < 2 * floor are empty: launch only levels 0..last
+    // (b40 1e9 field, chunk 1e6, floor 250: 12 launches instead of 23).
+    u32 last = 0;
+    while (last < 22 && ((p.chunk + (1ull << last) - 1) >> last) >= 2 * p.floor_size) last++;
+    // Level d holds <= nchunks * 2^d nodes: size its grid to that (the first
+    // levels are a few thousand lanes), capped at 8 workgroups per CU.
+    for (u32 level = 0; level <= last; level++) {
+        const u64 nodes = level < 40 ? nchunks << level : ~0ull;
+        u64 grid = (nodes + 255) / 256;
+        const u64 cap = (u64)num_cus * 8;
+        if (grid > cap || nodes >> level != nchunks) grid = cap;
+        hipLaunchKernelGGL((msd_level_kernel<G>), dim3((u32)grid), dim3(256), 0, s, p, level, g);
+    }
     return hipGetLastError();
 }
 

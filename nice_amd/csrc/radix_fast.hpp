@@ -1,0 +1,225 @@
+// radix_fast.hpp -- in-range fast paths for the niceonly kernels (b40/50/80).
+//
+// Inside a base's valid range n^2 and n^3 have exactly D2 and D3 base-b digits
+// (base_range.rs:14-32), so both fit fixed radix-B = b^2 limb arrays sized at
+// compile time.  Converting n to NX radix-B limbs and multiplying limb-wise
+// (every column sum < 2^32, so u32 arithmetic throughout) replaces the generic
+// path's chunked long division of 8- and 12-word numbers by b^E: the digit
+// pairs fall out of the limbs, and the dependent chains are a few steps long
+// instead of hundreds.  Used by
+//   * is_nice_fast      == get_is_nice (client_process.rs:222-253): n^2 then
+//                          n^3, least significant digit first, stop at the
+//                          first repeat;
+//   * msd_skippable_fast == has_duplicate_msd_prefix (msd_prefix_filter.rs:
+//                          382-563) incl. Filter C, for [first, last] in range.
+// Both agree bit-for-bit with the generic device functions (nice_device.hpp,
+// niceonly.hip) on in-range input; the GPU parity tests compare the candidate
+// sets and nice lists against the CPU path.
+#pragma once
+
+#include "nice_device.hpp"
+
+namespace nice {
+
+template <int BASE>
+struct Radix {
+    static constexpr u32 B = (u32)BASE * BASE;
+    static constexpr int k = BASE / 5, r5 = BASE % 5;
+    static constexpr int D2 = r5 == 0 ? 2 * k : (r5 == 4 ? 2 * k + 2 : 2 * k + 1);
+    static constexpr int D3 = r5 == 0 ? 3 * k : (r5 == 2 ? 3 * k + 1 : 3 * k + 2);
+    static constexpr int DN = r5 == 0 ? k : k + 1;
+    static constexpr int NX = cdiv(DN, 2), NS = cdiv(D2, 2), NC = cdiv(D3, 2);
+    static constexpr int MW = (BASE + 31) / 32;
+    static constexpr bool FITS64 = []() {
+        unsigned long long v = 1;
+        for (int i = 0; i < NX; i++) {
+            if (v > ~0ull / B) return false;
+            v *= B;
+        }
+        return true;
+    }();
+    // column sums: NX * (B-1)^2 (square) and NX * (B-1)^2 (cube, S limbs < B)
+    static_assert((unsigned long long)NX * (B - 1) * (B - 1) + B < (1ull << 32), "u32 columns");
+};
+
+template <int MW>
+__device__ __forceinline__ u32 mset(u32 (&m)[MW], u32 d) {
+    u32 dup = 0;
+#pragma unroll
+    for (int w = 0; w < MW; w++) {
+        const u32 bit = (d >> 5) == (u32)w ? 1u << (d & 31) : 0u;
+        dup |= m[w] & bit;
+        m[w] |= bit;
+    }
+    return dup;
+}
+template <int MW>
+__device__ __forceinline__ bool moverlap(const u32 (&a)[MW], const u32 (&b)[MW]) {
+    u32 o = 0;
+#pragma unroll
+    for (int w = 0; w < MW; w++) o |= a[w] & b[w];
+    return o != 0;
+}
+
+// n (in range, < B^NX) as NX radix-B limbs.
+template <int BASE>
+__device__ __forceinline__ void to_limbs(u64 lo, u64 hi, u32 (&X)[Radix<BASE>::NX]) {
+    constexpr u32 B = Radix<BASE>::B;
+    if constexpr (Radix<BASE>::FITS64) {  // n < B^NX < 2^64 (b40, b50)
+        (void)hi;
+        u64 v = lo;
+#pragma unroll
+        for (int j = 0; j < Radix<BASE>::NX; j++) {
+            const u64 q = v / B;
+            X[j] = (u32)(v - q * B);
+            v = q;
+        }
+    } else {
+        u32 w[4] = {(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
+#pragma unroll
+        for (int j = 0; j < Radix<BASE>::NX; j++) {
+            u64 rem = 0;
+#pragma unroll
+            for (int q = 3; q >= 0; q--) {
+                const u64 cur = (rem << 32) | w[q];
+                w[q] = (u32)(cur / B);
+                rem = cur - (u64)w[q] * B;
+            }
+            X[j] = (u32)rem;
+        }
+    }
+}
+
+// S = X^2 (NS limbs), C = S * X (NC limbs), normalised radix B.
+template <int BASE>
+__device__ __forceinline__ void square_limbs(const u32 (&X)[Radix<BASE>::NX], u32 (&S)[Radix<BASE>::NS]) {
+    using R = Radix<BASE>;
+    u32 acc[2 * R::NX];
+#pragma unroll
+    for (int t = 0; t < 2 * R::NX; t++) acc[t] = 0;
+#pragma unroll
+    for (int i = 0; i < R::NX; i++)
+#pragma unroll
+        for (int j = 0; j < R::NX; j++) acc[i + j] += X[i] * X[j];
+    u32 cy = 0;
+#pragma unroll
+    for (int t = 0; t < R::NS; t++) {
+        const u32 v = (t < 2 * R::NX ? acc[t] : 0u) + cy;
+        cy = v / R::B;
+        S[t] = v - cy * R::B;
+    }
+}
+template <int BASE>
+__device__ __forceinline__ void cube_limbs(const u32 (&S)[Radix<BASE>::NS], const u32 (&X)[Radix<BASE>::NX],
+                                           u32 (&C)[Radix<BASE>::NC]) {
+    using R = Radix<BASE>;
+    u32 acc[R::NS + R::NX];
+#pragma unroll
+    for (int t = 0; t < R::NS + R::NX; t++) acc[t] = 0;
+#pragma unroll
+    for (int i = 0; i < R::NS; i++)
+#pragma unroll
+        for (int j = 0; j < R::NX; j++) acc[i + j] += S[i] * X[j];
+    u32 cy = 0;
+#pragma unroll
+    for (int t = 0; t < R::NC; t++) {
+        const u32 v = (t < R::NS + R::NX ? acc[t] : 0u) + cy;
+        cy = v / R::B;
+        C[t] = v - cy * R::B;
+    }
+}
+
+// Digits of limb array A (D digits, LSD first) into m; false at the first repeat.
+template <int BASE, int N>
+__device__ __forceinline__ bool scan_limbs(const u32 (&A)[N], int D, u32 (&m)[Radix<BASE>::MW]) {
+#pragma unroll
+    for (int t = 0; t < N; t++) {
+        const u32 d1 = A[t] / BASE, d0 = A[t] - d1 * BASE;
+        if (mset(m, d0)) return false;
+        if (2 * t + 1 < D && mset(m, d1)) return false;
+    }
+    return true;
+}
+
+template <int BASE>
+__device__ __forceinline__ bool is_nice_fast(u64 lo, u64 hi) {
+    using R = Radix<BASE>;
+    u32 X[R::NX], S[R::NS];
+    to_limbs<BASE>(lo, hi, X);
+    square_limbs<BASE>(X, S);
+    u32 m[R::MW];
+#pragma unroll
+    for (int w = 0; w < R::MW; w++) m[w] = 0;
+    if (!scan_limbs<BASE>(S, R::D2, m)) return false;
+    u32 C[R::NC];
+    cube_limbs<BASE>(S, X, C);
+    return scan_limbs<BASE>(C, R::D3, m);
+}
+
+// Common most-significant prefix of two D-digit limb arrays: its digit mask
+// and whether a digit repeats inside it.  Limbs are walked from the top (fully
+// unrolled, static indices); the walk stops at the first differing digit.
+template <int BASE, int N>
+__device__ __forceinline__ void msd_prefix(const u32 (&F)[N], const u32 (&L)[N], int D,
+                                           u32 (&m)[Radix<BASE>::MW], u32 &dup) {
+#pragma unroll
+    for (int w = 0; w < Radix<BASE>::MW; w++) m[w] = 0;
+    dup = 0;
+    bool live = true;
+#pragma unroll
+    for (int t = N - 1; t >= 0; t--) {
+        if (live) {
+            const u32 f = F[t], l = L[t];
+            const u32 fh = f / BASE, lh = l / BASE;
+            if (2 * t + 1 < D) {  // high digit of the limb (absent above the top digit)
+                if (fh != lh) live = false;
+                else dup |= mset(m, fh);
+            }
+            if (live) {
+                if (f != l) live = false;  // high digits equal, so the low ones differ
+                else dup |= mset(m, f - fh * BASE);
+            }
+        }
+    }
+}
+
+// has_duplicate_msd_prefix on [first, last], both in range (equal digit counts).
+template <int BASE>
+__device__ __forceinline__ bool msd_skippable_fast(u64 f_lo, u64 f_hi, u64 l_lo, u64 l_hi) {
+    using R = Radix<BASE>;
+    u32 Xf[R::NX], Xl[R::NX], Sf[R::NS], Sl[R::NS];
+    to_limbs<BASE>(f_lo, f_hi, Xf);
+    to_limbs<BASE>(l_lo, l_hi, Xl);
+    square_limbs<BASE>(Xf, Sf);
+    square_limbs<BASE>(Xl, Sl);
+    u32 msq[R::MW], dsq;
+    msd_prefix<BASE>(Sf, Sl, R::D2, msq, dsq);
+    if (dsq) return true;
+    u32 Cf[R::NC], Cl[R::NC];
+    cube_limbs<BASE>(Sf, Xf, Cf);
+    cube_limbs<BASE>(Sl, Xl, Cl);
+    u32 mcu[R::MW], dcu;
+    msd_prefix<BASE>(Cf, Cl, R::D3, mcu, dcu);
+    if (dcu) return true;
+    if (moverlap(msq, mcu)) return true;
+    // Filter C (msd_prefix_filter.rs:461-559): first / b^2 == last / b^2, with
+    // first's two lowest digits of n^2 and n^3.
+    u32 diff = 0;
+#pragma unroll
+    for (int j = 1; j < R::NX; j++) diff |= Xf[j] ^ Xl[j];
+    if (diff == 0) {
+        u32 ms[R::MW], mc[R::MW];
+#pragma unroll
+        for (int w = 0; w < R::MW; w++) ms[w] = mc[w] = 0;
+        u32 ds = mset(ms, Sf[0] % BASE);
+        ds |= mset(ms, Sf[0] / BASE);
+        u32 dc = mset(mc, Cf[0] % BASE);
+        dc |= mset(mc, Cf[0] / BASE);
+        if (moverlap(msq, ms) || moverlap(mcu, mc) || moverlap(msq, mc) || moverlap(mcu, ms) || ds ||
+            dc || moverlap(ms, mc))
+            return true;
+    }
+    return false;
+}
+
+}  // namespace nice
