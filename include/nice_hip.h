@@ -145,6 +145,19 @@ int nice_msd_skippable(uint64_t start_lo, uint64_t start_hi, uint64_t end_lo, ui
 int nice_stride_table(uint32_t base, uint32_t k, uint64_t *modulus, uint32_t *residues,
                       size_t cap, size_t *n_out);
 
+/* Test hooks (no device needed): the in-range fast paths of the niceonly
+ * kernels (radix_fast.hpp) evaluated on the host, bases 40/50/80 with n (and
+ * [start, end)) inside the base's valid range.  is_nice: 1/0 like get_is_nice
+ * (client_process.rs:222-253); msd: 1/0 like has_duplicate_msd_prefix on
+ * [start, end - 1] (msd_prefix_filter.rs:382-563).  NICE_ERR_INVALID otherwise. */
+int nice_check_is_nice_inrange(uint32_t base, uint64_t n_lo, uint64_t n_hi);
+int nice_check_msd_skippable_inrange(uint32_t base, uint64_t start_lo, uint64_t start_hi,
+                                     uint64_t end_lo, uint64_t end_hi);
+/* Limb-count cuts of the production FD kernel (fd2_detailed.hip): the n at
+ * which a segment ending there needs a wider (D1, E1, E2) limb layout.  Writes
+ * (lo, hi) pairs, returns the count via *n_out.  Bases without an FD kernel: 0. */
+int nice_fd_segment_cuts(uint32_t base, uint64_t *out, size_t cap, size_t *n_out);
+
 /* Diagnostics: per-n results of the device functions the kernels use. */
 int nice_debug_unique_counts(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t count,
                              uint32_t base, uint32_t *out);

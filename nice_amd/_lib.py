@@ -27,7 +27,8 @@ EXPORTS = (
     "nice_near_miss_cutoff", "nice_gpu_batch_size", "nice_processing_chunk_size",
     "nice_gpu_supports_base", "nice_fd_kernel_base", "nice_msd_valid_ranges",
     "nice_msd_skippable", "nice_stride_table", "nice_debug_unique_counts",
-    "nice_debug_is_nice",
+    "nice_debug_is_nice", "nice_check_is_nice_inrange", "nice_check_msd_skippable_inrange",
+    "nice_fd_segment_cuts",
 )
 
 
@@ -112,6 +113,9 @@ def lib():
         "nice_stride_table": ([u32, u32, P64, P32, sz, PSZ], i32),
         "nice_debug_unique_counts": ([vp, P64, u32, u32, P32], i32),
         "nice_debug_is_nice": ([vp, P64, u32, u32, P32], i32),
+        "nice_check_is_nice_inrange": ([u32, u64, u64], i32),
+        "nice_check_msd_skippable_inrange": ([u32, u64, u64, u64, u64], i32),
+        "nice_fd_segment_cuts": ([u32, P64, sz, PSZ], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -540,6 +540,10 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         const u64 per_lane = (cnt + lanes - 1) / lanes;
         const u64 units_per_lane = (per_lane + P::B - 1) / P::B < 3 ? 3 : (per_lane + P::B - 1) / P::B;
         u64 chunk = (cnt + lanes * units_per_lane - 1) / (lanes * units_per_lane);
+        // A lane's init (radix-B conversion, products) costs about ten steps:
+        // small fields use fewer lanes with >= 32 numbers each instead of
+        // one number per lane.
+        if (chunk < 32) chunk = cnt < 32 ? cnt : 32;
         if (chunk < 1) chunk = 1;
         if (chunk > P::B) chunk = P::B;
         // Odd chunks: lane l of a wave then sits at n mod B = r0 + chunk * l,
@@ -676,6 +680,13 @@ static hipError_t launch_segment(const DetailedLaunch &p, int num_cus, hipStream
 }  // namespace fd2
 
 bool fd2_supported(uint32_t base) { return base == 40 || base == 50 || base == 80; }
+
+size_t fd2_cuts(uint32_t base, unsigned __int128 *out, size_t cap) {
+    if (!fd2_supported(base)) return 0;
+    const fd2::BaseThresholds &t = fd2::thresholds(base);
+    for (size_t i = 0; i < t.cuts.size() && i < cap; i++) out[i] = t.cuts[i];
+    return t.cuts.size();
+}
 
 // In-range segment [start, start + count): split at the limb-count cuts, one
 // launch (plus a tail launch) per piece.

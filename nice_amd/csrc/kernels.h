@@ -32,6 +32,8 @@ hipError_t launch_detailed_fd(const DetailedLaunch &p, int num_cus, hipStream_t 
 // Production FD kernel (fd2_detailed.hip): bases 40, 50, 80, in-range segments.
 bool fd2_supported(uint32_t base);
 hipError_t launch_detailed_fd2(const DetailedLaunch &p, int num_cus, hipStream_t s);
+// The n where fd2's per-segment limb layout changes (ascending).
+size_t fd2_cuts(uint32_t base, unsigned __int128 *out, size_t cap);
 // Generic per-n kernel: any base 2..128, any n < 2^128.
 hipError_t launch_detailed_generic(const DetailedLaunch &p, int num_cus, hipStream_t s);
 

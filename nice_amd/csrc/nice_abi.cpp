@@ -25,6 +25,7 @@
 #include "../../include/nice_hip.h"
 #include "host_math.hpp"
 #include "kernels.h"
+#include "radix_fast.hpp"
 
 using nice::u128;
 
@@ -458,6 +459,45 @@ int nice_debug_is_nice(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t count, u
     HIPCHK(hipMemcpy(out, du, (size_t)count * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipFree(dn));
     HIPCHK(hipFree(du));
+    return NICE_OK;
+}
+
+int nice_check_is_nice_inrange(uint32_t base, uint64_t lo, uint64_t hi) {
+    u128 rs, re;
+    const u128 n = mk(lo, hi);
+    if (!nice::fd2_supported(base) || nice::base_range(base, rs, re) != 1 || n < rs || n >= re)
+        return fail(NICE_ERR_INVALID, "n outside the base's valid range (or base not 40/50/80)");
+    switch (base) {
+    case 40: return nice::is_nice_fast<40>(lo, hi) ? 1 : 0;
+    case 50: return nice::is_nice_fast<50>(lo, hi) ? 1 : 0;
+    default: return nice::is_nice_fast<80>(lo, hi) ? 1 : 0;
+    }
+}
+
+int nice_check_msd_skippable_inrange(uint32_t base, uint64_t slo, uint64_t shi, uint64_t elo,
+                                     uint64_t ehi) {
+    u128 rs, re;
+    const u128 s = mk(slo, shi), e = mk(elo, ehi);
+    if (!nice::fd2_supported(base) || nice::base_range(base, rs, re) != 1 || s < rs || e > re || s >= e)
+        return fail(NICE_ERR_INVALID, "range outside the base's valid range (or base not 40/50/80)");
+    if (e - s == 1) return 0;  // a single number is never skipped (msd_prefix_filter.rs:395)
+    const u128 l = e - 1;
+    const uint64_t llo = lo64(l), lhi = hi64(l);
+    switch (base) {
+    case 40: return nice::msd_skippable_fast<40>(slo, shi, llo, lhi) ? 1 : 0;
+    case 50: return nice::msd_skippable_fast<50>(slo, shi, llo, lhi) ? 1 : 0;
+    default: return nice::msd_skippable_fast<80>(slo, shi, llo, lhi) ? 1 : 0;
+    }
+}
+
+int nice_fd_segment_cuts(uint32_t base, uint64_t *out, size_t cap, size_t *n_out) {
+    std::vector<u128> c(8);
+    const size_t n = nice::fd2_cuts(base, c.data(), c.size());
+    for (size_t i = 0; i < n && i < cap; i++) {
+        out[2 * i] = lo64(c[i]);
+        out[2 * i + 1] = hi64(c[i]);
+    }
+    if (n_out) *n_out = n;
     return NICE_OK;
 }
 

@@ -14,7 +14,9 @@
 //                          382-563) incl. Filter C, for [first, last] in range.
 // Both agree bit-for-bit with the generic device functions (nice_device.hpp,
 // niceonly.hip) on in-range input; the GPU parity tests compare the candidate
-// sets and nice lists against the CPU path.
+// sets and nice lists against the CPU path.  The same templates also compile
+// for the host (plain integer C++), exported as test hooks so the CPU suite
+// checks them against the oracle on random in-range inputs.
 #pragma once
 
 #include "nice_device.hpp"
@@ -43,7 +45,7 @@ struct Radix {
 };
 
 template <int MW>
-__device__ __forceinline__ u32 mset(u32 (&m)[MW], u32 d) {
+__host__ __device__ __forceinline__ u32 mset(u32 (&m)[MW], u32 d) {
     u32 dup = 0;
 #pragma unroll
     for (int w = 0; w < MW; w++) {
@@ -54,7 +56,7 @@ __device__ __forceinline__ u32 mset(u32 (&m)[MW], u32 d) {
     return dup;
 }
 template <int MW>
-__device__ __forceinline__ bool moverlap(const u32 (&a)[MW], const u32 (&b)[MW]) {
+__host__ __device__ __forceinline__ bool moverlap(const u32 (&a)[MW], const u32 (&b)[MW]) {
     u32 o = 0;
 #pragma unroll
     for (int w = 0; w < MW; w++) o |= a[w] & b[w];
@@ -63,7 +65,7 @@ __device__ __forceinline__ bool moverlap(const u32 (&a)[MW], const u32 (&b)[MW])
 
 // n (in range, < B^NX) as NX radix-B limbs.
 template <int BASE>
-__device__ __forceinline__ void to_limbs(u64 lo, u64 hi, u32 (&X)[Radix<BASE>::NX]) {
+__host__ __device__ __forceinline__ void to_limbs(u64 lo, u64 hi, u32 (&X)[Radix<BASE>::NX]) {
     constexpr u32 B = Radix<BASE>::B;
     if constexpr (Radix<BASE>::FITS64) {  // n < B^NX < 2^64 (b40, b50)
         (void)hi;
@@ -92,7 +94,7 @@ __device__ __forceinline__ void to_limbs(u64 lo, u64 hi, u32 (&X)[Radix<BASE>::N
 
 // S = X^2 (NS limbs), C = S * X (NC limbs), normalised radix B.
 template <int BASE>
-__device__ __forceinline__ void square_limbs(const u32 (&X)[Radix<BASE>::NX], u32 (&S)[Radix<BASE>::NS]) {
+__host__ __device__ __forceinline__ void square_limbs(const u32 (&X)[Radix<BASE>::NX], u32 (&S)[Radix<BASE>::NS]) {
     using R = Radix<BASE>;
     u32 acc[2 * R::NX];
 #pragma unroll
@@ -110,7 +112,7 @@ __device__ __forceinline__ void square_limbs(const u32 (&X)[Radix<BASE>::NX], u3
     }
 }
 template <int BASE>
-__device__ __forceinline__ void cube_limbs(const u32 (&S)[Radix<BASE>::NS], const u32 (&X)[Radix<BASE>::NX],
+__host__ __device__ __forceinline__ void cube_limbs(const u32 (&S)[Radix<BASE>::NS], const u32 (&X)[Radix<BASE>::NX],
                                            u32 (&C)[Radix<BASE>::NC]) {
     using R = Radix<BASE>;
     u32 acc[R::NS + R::NX];
@@ -131,7 +133,7 @@ __device__ __forceinline__ void cube_limbs(const u32 (&S)[Radix<BASE>::NS], cons
 
 // Digits of limb array A (D digits, LSD first) into m; false at the first repeat.
 template <int BASE, int N>
-__device__ __forceinline__ bool scan_limbs(const u32 (&A)[N], int D, u32 (&m)[Radix<BASE>::MW]) {
+__host__ __device__ __forceinline__ bool scan_limbs(const u32 (&A)[N], int D, u32 (&m)[Radix<BASE>::MW]) {
 #pragma unroll
     for (int t = 0; t < N; t++) {
         const u32 d1 = A[t] / BASE, d0 = A[t] - d1 * BASE;
@@ -142,7 +144,7 @@ __device__ __forceinline__ bool scan_limbs(const u32 (&A)[N], int D, u32 (&m)[Ra
 }
 
 template <int BASE>
-__device__ __forceinline__ bool is_nice_fast(u64 lo, u64 hi) {
+__host__ __device__ __forceinline__ bool is_nice_fast(u64 lo, u64 hi) {
     using R = Radix<BASE>;
     u32 X[R::NX], S[R::NS];
     to_limbs<BASE>(lo, hi, X);
@@ -160,7 +162,7 @@ __device__ __forceinline__ bool is_nice_fast(u64 lo, u64 hi) {
 // and whether a digit repeats inside it.  Limbs are walked from the top (fully
 // unrolled, static indices); the walk stops at the first differing digit.
 template <int BASE, int N>
-__device__ __forceinline__ void msd_prefix(const u32 (&F)[N], const u32 (&L)[N], int D,
+__host__ __device__ __forceinline__ void msd_prefix(const u32 (&F)[N], const u32 (&L)[N], int D,
                                            u32 (&m)[Radix<BASE>::MW], u32 &dup) {
 #pragma unroll
     for (int w = 0; w < Radix<BASE>::MW; w++) m[w] = 0;
@@ -185,7 +187,7 @@ __device__ __forceinline__ void msd_prefix(const u32 (&F)[N], const u32 (&L)[N],
 
 // has_duplicate_msd_prefix on [first, last], both in range (equal digit counts).
 template <int BASE>
-__device__ __forceinline__ bool msd_skippable_fast(u64 f_lo, u64 f_hi, u64 l_lo, u64 l_hi) {
+__host__ __device__ __forceinline__ bool msd_skippable_fast(u64 f_lo, u64 f_hi, u64 l_lo, u64 l_hi) {
     using R = Radix<BASE>;
     u32 Xf[R::NX], Xl[R::NX], Sf[R::NS], Sl[R::NS];
     to_limbs<BASE>(f_lo, f_hi, Xf);

@@ -6,6 +6,7 @@
   reference's golden vectors bit for bit;
 - without a GPU, context creation fails loudly (no CPU fallback).
 """
+import ctypes
 import os
 import random
 import re
@@ -119,3 +120,90 @@ def test_no_gpu_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(N.NiceError):
         N.GpuContext(0)
+
+
+# --- host-evaluated fast paths of the device kernels (no GPU needed) --------
+
+def _fd2_cuts_py(base):
+    """n where a segment ending at e needs more radix-b^2 limbs for D1 = 2e+1,
+    E1 = 3e^2+3e+1 or E2 = 6e+6 (fd2_detailed.hip), by exact integer search."""
+    B = base * base
+
+    def limbs(x):
+        k = 0
+        while x >= B ** k:
+            k += 1
+        return k
+
+    def combo(e):
+        return (limbs(2 * e + 1), limbs(3 * e * e + 3 * e + 1), limbs(6 * e + 6))
+
+    s, e = O.base_range(base)
+    cuts, a = [], s
+    while combo(a + 1) != combo(e):
+        lo, hi, cur = a + 1, e, combo(a + 1)
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if combo(mid) == cur:
+                lo = mid + 1
+            else:
+                hi = mid
+        cuts.append(lo - 1)
+        a = lo - 1
+    return cuts
+
+
+@pytest.mark.parametrize("base", [40, 50, 80])
+def test_fd_segment_cuts_match_python(base):
+    L = _lib.lib()
+    buf = (ctypes.c_uint64 * 16)()
+    n = ctypes.c_size_t()
+    assert L.nice_fd_segment_cuts(base, buf, 8, ctypes.byref(n)) == 0
+    got = [buf[2 * i] | (buf[2 * i + 1] << 64) for i in range(n.value)]
+    assert got == _fd2_cuts_py(base) and len(got) == 2
+    assert L.nice_fd_segment_cuts(10, buf, 8, ctypes.byref(n)) == 0 and n.value == 0
+
+
+def _split(x):
+    return x & ((1 << 64) - 1), x >> 64
+
+
+@pytest.mark.parametrize("base", [40, 50, 80])
+def test_is_nice_fast_path_matches_oracle(base):
+    """radix_fast.hpp's is_nice_fast (the niceonly kernel's in-range check)
+    against the oracle's get_is_nice on random in-range n, plus near-nice n
+    (the ones that reach the cube scan)."""
+    L = _lib.lib()
+    rng = random.Random(base)
+    s, e = O.base_range(base)
+    ns = [s, e - 1] + [rng.randrange(s, e) for _ in range(3000)]
+    deep = [n for n in (rng.randrange(s, e) for _ in range(40000)) if O.scan_depth(n, base) > base // 3]
+    for n in ns + deep[:500]:
+        assert L.nice_check_is_nice_inrange(base, *_split(n)) == int(O.is_nice(n, base)), n
+    assert L.nice_check_is_nice_inrange(base, *_split(s - 1)) == _lib.NICE_ERR_INVALID
+
+
+@pytest.mark.parametrize("base", [40, 50, 80])
+def test_msd_fast_path_matches_oracle(base):
+    """radix_fast.hpp's msd_skippable_fast (the device MSD filter's in-range
+    check) against the oracle's has_duplicate_msd_prefix, on random ranges of
+    every scale, including Filter C ranges (first / b^2 == last / b^2)."""
+    L = _lib.lib()
+    rng = random.Random(1000 + base)
+    s, e = O.base_range(base)
+    B = base * base
+    cases = []
+    for _ in range(1500):
+        size = 10 ** rng.uniform(0, 9)
+        a = rng.randrange(s, e - int(size) - 1)
+        cases.append((a, a + max(1, int(size))))
+    for _ in range(1500):  # inside one b^2 block: Filter C applies
+        blk = rng.randrange(s // B + 1, e // B - 1) * B
+        a = blk + rng.randrange(B - 2)
+        cases.append((a, rng.randrange(a + 1, blk + B + 1)))
+    hits = 0
+    for a, b in cases:
+        want = int(O.has_duplicate_msd_prefix(a, b, base))
+        hits += want
+        assert L.nice_check_msd_skippable_inrange(base, *_split(a), *_split(b)) == want, (a, b)
+    assert 0 < hits < len(cases)
