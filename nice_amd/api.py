@@ -130,6 +130,11 @@ class GpuContext:
         check(lib().nice_ctx_create(arr, len(devices), ctypes.byref(h)))
         self._h = h
         self.devices = list(devices)
+        # Reused host output buffer (grown on NICE_ERR_CAPACITY): allocating a
+        # zeroed 64K-entry ctypes array per call cost ~0.1 ms of host time.
+        self._out = None
+        self._out_cap = 0
+        self._hist = {}
 
     @classmethod
     def new(cls, device_ordinal: int = 0) -> "GpuContext":
@@ -146,17 +151,26 @@ class GpuContext:
         except Exception:
             pass
 
+    def _out_buf(self, cap):
+        if cap > self._out_cap:
+            self._out = (_lib.nice_number * cap)()
+            self._out_cap = cap
+        return self._out
+
     def kernel_stats(self, device_index: int = 0) -> KernelStats:
         s = _lib.nice_kernel_stats()
         check(lib().nice_last_kernel_stats(self._h, device_index, s))
         return KernelStats(s.kernel_ms, s.launches, bool(s.fd_kernel), s.numbers)
 
     # -- detailed -------------------------------------------------------------
-    def detailed_raw(self, start: int, end: int, base: int, cap: int = 1 << 16):
+    def detailed_raw(self, start: int, end: int, base: int, cap: int = 0):
         """Histogram (base+1 bins) and near-miss list [(n, u)] ascending."""
-        hist = (ctypes.c_uint64 * (base + 1))()
+        hist = self._hist.get(base)
+        if hist is None:
+            hist = self._hist[base] = (ctypes.c_uint64 * (base + 1))()
+        cap = max(cap, self._out_cap, 1024)
         while True:
-            out = (_lib.nice_number * max(cap, 1))()
+            out = self._out_buf(cap)
             n = ctypes.c_size_t()
             rc = lib().nice_process_range_detailed(self._h, *_split(start), *_split(end), base,
                                                    hist, out, cap, n)
@@ -171,12 +185,13 @@ class GpuContext:
     # -- niceonly -------------------------------------------------------------
     def niceonly_raw(self, start: int, end: int, base: int, msd_floor: int = 0,
                      chunk_size: int = 0, threads: int = 0, stride_k: int = 0,
-                     msd_where: str = "auto", cap: int = 1 << 16):
+                     msd_where: str = "auto", cap: int = 0):
         where = {"auto": 0, "host": 1, "device": 2}[msd_where]
         opts = _lib.nice_niceonly_opts(msd_floor, chunk_size, threads, stride_k, where, 0)
         st = _lib.nice_niceonly_stats()
+        cap = max(cap, self._out_cap, 1024)
         while True:
-            out = (_lib.nice_number * max(cap, 1))()
+            out = self._out_buf(cap)
             n = ctypes.c_size_t()
             rc = lib().nice_process_range_niceonly_ex(self._h, *_split(start), *_split(end), base,
                                                       opts, out, cap, n, st)

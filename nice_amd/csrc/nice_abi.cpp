@@ -31,6 +31,8 @@ using nice::u128;
 
 namespace {
 
+constexpr size_t kStateBytes = 129 * 8 + 2 * 4;  // per-device hist bins + list counters
+
 thread_local std::string g_err;
 
 int fail(int code, const std::string &msg) {
@@ -75,8 +77,8 @@ struct Device {
     int num_cus = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_done = nullptr;
-    uint64_t *d_hist = nullptr;   // 129 bins
-    uint32_t *d_count = nullptr;  // list counters [0] detailed, [1] niceonly
+    uint64_t *d_hist = nullptr;   // 129 bins, then d_count
+    uint32_t *d_count = nullptr;  // list counters [0] detailed, [1] niceonly (inside d_hist's block)
     uint64_t *d_list_n = nullptr;
     uint32_t *d_list_u = nullptr;
     uint32_t list_cap = 0;
@@ -170,10 +172,11 @@ int device_init(Device &d, int id) {
     HIPCHK(hipEventCreate(&d.ev0));
     HIPCHK(hipEventCreate(&d.ev1));
     HIPCHK(hipEventCreateWithFlags(&d.ev_done, hipEventDisableTiming));
-    HIPCHK(hipMalloc(&d.d_hist, 129 * 8));
-    HIPCHK(hipMalloc(&d.d_count, 2 * 4));
-    HIPCHK(hipHostMalloc(&d.h_hist, 129 * 8, hipHostMallocDefault));
-    HIPCHK(hipHostMalloc(&d.h_count, 2 * 4, hipHostMallocDefault));
+    // hist bins and list counters in one block: one memset and one copy per field.
+    HIPCHK(hipMalloc(&d.d_hist, kStateBytes));
+    d.d_count = (uint32_t *)(d.d_hist + 129);
+    HIPCHK(hipHostMalloc(&d.h_hist, kStateBytes, hipHostMallocDefault));
+    d.h_count = (uint32_t *)(d.h_hist + 129);
     int rc = ensure_list(d, kInitialListCap);
     if (rc) return rc;
     return NICE_OK;
@@ -198,11 +201,9 @@ void device_free(Device &d) {
     if (d.msd.counters) (void)hipFree(d.msd.counters);
     if (d.msd.h_counters) (void)hipHostFree(d.msd.h_counters);
     (void)hipFree(d.d_hist);
-    (void)hipFree(d.d_count);
     (void)hipFree(d.d_list_n);
     (void)hipFree(d.d_list_u);
     (void)hipHostFree(d.h_hist);
-    (void)hipHostFree(d.h_count);
     (void)hipEventDestroy(d.ev0);
     (void)hipEventDestroy(d.ev1);
     (void)hipEventDestroy(d.ev_done);
@@ -363,16 +364,14 @@ int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start
         d.last = nice_kernel_stats{};
         if (bounds[i] >= bounds[i + 1]) continue;
         HIPCHK(hipSetDevice(d.id));
-        HIPCHK(hipMemsetAsync(d.d_hist, 0, 129 * 8, d.stream));
-        HIPCHK(hipMemsetAsync(d.d_count, 0, 8, d.stream));
+        HIPCHK(hipMemsetAsync(d.d_hist, 0, kStateBytes, d.stream));
         HIPCHK(hipEventRecord(d.ev0, d.stream));
         bool used_fd = false;
         uint64_t fdc = 0;
         int rc = enqueue_detailed(d, bounds[i], bounds[i + 1], base, used_fd, fdc);
         if (rc) return rc;
         HIPCHK(hipEventRecord(d.ev1, d.stream));
-        HIPCHK(hipMemcpyAsync(d.h_hist, d.d_hist, (base + 1) * 8, hipMemcpyDeviceToHost, d.stream));
-        HIPCHK(hipMemcpyAsync(d.h_count, d.d_count, 4, hipMemcpyDeviceToHost, d.stream));
+        HIPCHK(hipMemcpyAsync(d.h_hist, d.d_hist, kStateBytes, hipMemcpyDeviceToHost, d.stream));
         HIPCHK(hipEventRecord(d.ev_done, d.stream));
         d.last.fd_kernel = used_fd;
         d.last.numbers = (uint64_t)(bounds[i + 1] - bounds[i]);
@@ -394,14 +393,12 @@ int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start
             // grow to the exact count and redo this shard.
             int rc = ensure_list(d, cnt);
             if (rc) return rc;
-            HIPCHK(hipMemsetAsync(d.d_hist, 0, 129 * 8, d.stream));
-            HIPCHK(hipMemsetAsync(d.d_count, 0, 8, d.stream));
+            HIPCHK(hipMemsetAsync(d.d_hist, 0, kStateBytes, d.stream));
             bool used_fd = false;
             uint64_t fdc = 0;
             rc = enqueue_detailed(d, bounds[i], bounds[i + 1], base, used_fd, fdc);
             if (rc) return rc;
-            HIPCHK(hipMemcpyAsync(d.h_hist, d.d_hist, (base + 1) * 8, hipMemcpyDeviceToHost, d.stream));
-            HIPCHK(hipMemcpyAsync(d.h_count, d.d_count, 4, hipMemcpyDeviceToHost, d.stream));
+            HIPCHK(hipMemcpyAsync(d.h_hist, d.d_hist, kStateBytes, hipMemcpyDeviceToHost, d.stream));
             HIPCHK(hipStreamSynchronize(d.stream));
             cnt = d.h_count[0];
             if (cnt > d.list_cap) return fail(NICE_ERR_HIP, "near-miss list overflow after resize");
@@ -618,7 +615,8 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
             HIPCHK(hipSetDevice(d.id));
             const u128 bs = s + (u128)bi * batch_n;
             const uint64_t bsize = (uint64_t)std::min<u128>(batch_n, e - bs);
-            HIPCHK(hipMemsetAsync(d.msd.counters, 0, 25 * 4, d.stream));
+            if (bi >= ctx->devs.size())  // first batch per device: zeroed above
+                HIPCHK(hipMemsetAsync(d.msd.counters, 0, 25 * 4, d.stream));
             nice::MsdLaunch mp{};
             mp.start_lo = lo64(bs);
             mp.start_hi = hi64(bs);
