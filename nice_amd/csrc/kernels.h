@@ -85,6 +85,7 @@ struct MsdLaunch {
     uint32_t R, M;
     uint32_t base;
     uint32_t in_range;            // the batch lies inside the base's valid range
+    uint32_t probe;               // timing experiments (NICE_MSD_PROBE): 1 no skip test, 2 no leaf stride math
 };
 // Enqueue the init + 22 level kernels (no host sync).
 hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s);

@@ -635,6 +635,7 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
             mp.M = (uint32_t)M;
             mp.base = base;
             mp.in_range = in_range;
+            mp.probe = getenv("NICE_MSD_PROBE") ? (uint32_t)atoi(getenv("NICE_MSD_PROBE")) : 0u;
             hipError_t err = nice::launch_msd_device(mp, d.num_cus, d.stream);
             if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("msd launch: ") + hipGetErrorString(err));
             nice::NiceonlyLaunch p{};
@@ -657,6 +658,11 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
                                   d.stream));
             HIPCHK(hipStreamSynchronize(d.stream));
             const uint32_t *c = d.msd.h_counters;
+            if (getenv("NICE_MSD_TRACE")) {  // level sizes of the last batch (diagnostics)
+                fprintf(stderr, "msd levels:");
+                for (int lv = 0; lv < 24; lv++) fprintf(stderr, " %u", c[lv]);
+                fprintf(stderr, " | leaves %u\n", c[26]);
+            }
             if (c[25])
                 return fail(NICE_ERR_CAPACITY, "device MSD queue overflow (msd_floor too small for "
                                                "chunk_size); use msd_where = host");

@@ -45,27 +45,31 @@ niceonly_kernel(NiceonlyLaunch p, G g) {
     const u32 gwave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const u32 nwaves = (gridDim.x * blockDim.x) >> 6;
     const u32 n_leaves = p.n_leaves_dev ? min(*p.n_leaves_dev, p.n_leaves) : p.n_leaves;
-    for (u32 base = gwave * 64; base < n_leaves; base += nwaves * 64) {
+    // LPW leaves per wave (lanes >= LPW carry count 0): at the CPU path's
+    // floor a leaf holds ~40 candidates, so 8 leaves keep a wave ~5 rounds
+    // deep and spread a 35k-leaf field over ~4400 waves instead of ~550.
+    constexpr u32 LPW = 8;
+    for (u32 base = gwave * LPW; base < n_leaves; base += nwaves * LPW) {
         const u32 li = base + lane;
         Leaf lf{0, 0, 0, 0};
-        if (li < n_leaves) lf = p.leaves[li];
+        if (lane < LPW && li < n_leaves) lf = p.leaves[li];
         // inclusive scan of counts across the wave
         u32 incl = lf.count;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
+        for (int o = 1; o < (int)LPW; o <<= 1) {
             u32 v = __shfl_up(incl, o);
             if (lane >= (u32)o) incl += v;
         }
         const u32 excl = incl - lf.count;
-        const u32 total = __shfl(incl, 63);
+        const u32 total = __shfl(incl, LPW - 1);
         for (u32 r0 = 0; r0 < total; r0 += 64) {
             const u32 k = r0 + lane;
-            // largest l with excl_l <= k (uniform 6-step search, all lanes active)
+            // largest l < LPW with excl_l <= k (uniform search, all lanes active)
             u32 lo = 0;
 #pragma unroll
-            for (u32 step = 32; step >= 1; step >>= 1) {
+            for (u32 step = LPW / 2; step >= 1; step >>= 1) {
                 const u32 e = __shfl(excl, lo + step);
-                if (lo + step < 64 && e <= k) lo += step;
+                if (lo + step < LPW && e <= k) lo += step;
             }
             const u32 j = k - __shfl(excl, lo);
             const u32 g0 = __shfl(lf.g0, lo);
@@ -210,9 +214,23 @@ __device__ bool msd_skippable(u64 f_lo, u64 f_hi, u64 l_lo, u64 l_hi, const G &g
     return false;
 }
 
-// Stride-index descriptor of [a, a + size), appended if it holds candidates.
-template <class G>
-__device__ void emit_leaf(u64 a_lo, u64 a_hi, u64 size, const MsdLaunch &p) {
+// Stride-index descriptor of [a, a + size): cycle base b0 = a - a mod M,
+// first residue index g0 and candidate count (stride_filter.rs:99-155).
+struct LeafDesc {
+    u64 b0_lo, b0_hi, count;
+    u32 g0;
+};
+template <u32 MC>
+__device__ __forceinline__ LeafDesc leaf_desc(u64 a_lo, u64 a_hi, u64 size, const MsdLaunch &p) {
+    if constexpr (MC != 0) {
+        // In-range b40 / b50 (n < 2^64) with the k = 2 stride modulus as a
+        // compile-time constant: u64 divisions by a constant.
+        const u64 a = a_lo, e = a_lo + size;
+        const u64 qa = a / MC, qe = e / MC;
+        const u32 ra = (u32)(a - qa * MC), re = (u32)(e - qe * MC);
+        const u32 g0 = p.ranks[ra], g1 = p.ranks[re];
+        return LeafDesc{a - ra, 0, (qe - qa) * p.R + g1 - g0, g0};
+    }
     u64 q_lo = a_lo, q_hi = a_hi;
     const u32 ra = divmod_u128(q_lo, q_hi, p.M);
     u64 e_lo = a_lo, e_hi = a_hi;
@@ -221,22 +239,36 @@ __device__ void emit_leaf(u64 a_lo, u64 a_hi, u64 size, const MsdLaunch &p) {
     const u32 re = divmod_u128(qe_lo, qe_hi, p.M);
     const u32 g0 = p.ranks[ra], g1 = p.ranks[re];
     // cycles between the two ends (< 2^64 / M for any batch)
-    const u64 dcyc = qe_lo - q_lo;
-    const u64 count = dcyc * p.R + g1 - g0;
-    if (count == 0) return;
-    const u32 pos = atomicAdd(&p.counters[24], 1u);
-    if (pos >= p.leaf_cap || count > 0xffffffffull) {
-        atomicOr(&p.counters[25], 1u);
-        return;
-    }
+    const u64 count = (qe_lo - q_lo) * p.R + g1 - g0;
     u64 b0_lo = a_lo, b0_hi = a_hi;
-    // b0 = a - ra  (u128 minus u32)
-    b0_hi -= (b0_lo < ra) ? 1 : 0;
+    b0_hi -= (b0_lo < ra) ? 1 : 0;  // b0 = a - ra (u128 minus u32)
     b0_lo -= ra;
-    p.leaves[pos] = Leaf{b0_lo, b0_hi, g0, (u32)count};
-    atomicAdd(&p.counters[26], 1u);
-    atomicAdd((unsigned long long *)(p.counters + 28), (unsigned long long)count);
-    atomicAdd((unsigned long long *)(p.counters + 30), (unsigned long long)size);
+    return LeafDesc{b0_lo, b0_hi, count, g0};
+}
+
+// Wave-level helpers (every lane of the wave calls them together).
+__device__ __forceinline__ u32 lane_rank(u64 mask) {
+    return __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u));
+}
+__device__ __forceinline__ u64 wave_sum(u64 v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+// Reserve `mine` slots per lane in counter *ctr with ONE atomic per wave;
+// returns this lane's first slot.
+__device__ __forceinline__ u32 wave_reserve(u32 *ctr, u32 mine) {
+    u32 incl = mine;
+    const u32 lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const u32 v = __shfl_up(incl, o);
+        if (lane >= (u32)o) incl += v;
+    }
+    const u32 total = __shfl(incl, 63);
+    u32 base = 0;
+    if (lane == 0 && total) base = atomicAdd(ctr, total);
+    return __shfl(base, 0) + incl - mine;
 }
 
 __global__ void msd_init_kernel(MsdLaunch p) {
@@ -251,44 +283,123 @@ __global__ void msd_init_kernel(MsdLaunch p) {
     if (blockIdx.x == 0 && threadIdx.x == 0) p.counters[0] = (u32)nchunks;
 }
 
-template <class G>
+// Reserve `mine` slots per thread of a 256-thread workgroup with ONE atomic
+// per workgroup (same-address atomics from every wave of the chip serialise in
+// L2: ~1000 per level cost ~40 us).  All threads must call it; `slots` is 4
+// words of LDS.  Returns this thread's first slot.
+__device__ __forceinline__ u32 block_reserve(u32 *ctr, u32 mine, u32 *slots) {
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u32 incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const u32 v = __shfl_up(incl, o);
+        if (lane >= (u32)o) incl += v;
+    }
+    if (lane == 63) slots[wave] = incl;
+    __syncthreads();
+    u32 before = 0, total = 0;
+#pragma unroll
+    for (u32 w = 0; w < 4; w++) {
+        const u32 t = slots[w];
+        before += w < wave ? t : 0u;
+        total += t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) slots[0] = total ? atomicAdd(ctr, total) : 0u;
+    __syncthreads();
+    const u32 base = slots[0];
+    __syncthreads();
+    return base + before + incl - mine;
+}
+
+template <class G, u32 MC>
 __global__ void __launch_bounds__(256)
 msd_level_kernel(MsdLaunch p, u32 level, G g) {
+    __shared__ u32 slots[4];
+    __shared__ unsigned long long stat[3];
+    if (threadIdx.x < 3) stat[threadIdx.x] = 0;
     const MsdNode *qin = p.q[level & 1];
     MsdNode *qout = p.q[(level + 1) & 1];
     const u32 n_in = p.counters[level];
-    for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n_in; i += gridDim.x * blockDim.x) {
-        const MsdNode nd = qin[i];
-        bool leaf = level >= 22 || nd.size <= p.floor_size;
-        if (!leaf) {
-            u64 l_lo = nd.lo, l_hi = nd.hi;
-            add_u128(l_lo, l_hi, nd.size - 1);
+    const u32 lane = threadIdx.x & 63;
+    // Workgroup-uniform loop: leaves and children are appended with one atomic
+    // per workgroup, statistics summed in LDS and added once at the end.
+    const u32 stride = gridDim.x * blockDim.x;
+    u64 n_st = 0, c_st = 0, s_st = 0;
+    for (u32 b0 = blockIdx.x * blockDim.x; b0 < n_in; b0 += stride) {
+        const u32 i = b0 + threadIdx.x;
+        u32 act = 0;  // 0 drop / idle, 1 leaf, 2 split
+        MsdNode nd{0, 0, 0, 0, 0};
+        if (i < n_in) {
+            nd = qin[i];
+            bool leaf = level >= 22 || nd.size <= p.floor_size;
             bool skip = false;
-            if (nd.size != 1) {
-                if constexpr (IsConst<G>::value) {
-                    skip = p.in_range ? msd_skippable_fast<IsConst<G>::base>(nd.lo, nd.hi, l_lo, l_hi)
-                                      : msd_skippable<G>(nd.lo, nd.hi, l_lo, l_hi, g);
-                } else {
-                    skip = msd_skippable<G>(nd.lo, nd.hi, l_lo, l_hi, g);
+            if (!leaf) {
+                u64 l_lo = nd.lo, l_hi = nd.hi;
+                add_u128(l_lo, l_hi, nd.size - 1);
+                if (nd.size != 1 && !(p.probe & 1)) {
+                    if constexpr (IsConst<G>::value) {
+                        skip = p.in_range ? msd_skippable_fast<IsConst<G>::base>(nd.lo, nd.hi, l_lo, l_hi)
+                                          : msd_skippable<G>(nd.lo, nd.hi, l_lo, l_hi, g);
+                    } else {
+                        skip = msd_skippable<G>(nd.lo, nd.hi, l_lo, l_hi, g);
+                    }
                 }
+                leaf = nd.size < 2 * p.floor_size;
             }
-            if (skip) continue;
-            leaf = nd.size < 2 * p.floor_size;
+            act = skip ? 0u : (leaf ? 1u : 2u);
         }
-        if (leaf) {
-            emit_leaf<G>(nd.lo, nd.hi, nd.size, p);
-        } else {
-            const u64 half = nd.size / 2;
-            const u32 pos = atomicAdd(&p.counters[level + 1], 2u);
-            if (pos + 1 >= p.q_cap) {
+        LeafDesc ld{0, 0, 0, 0};
+        if (act == 1 && (p.probe & 2)) {
+            ld = LeafDesc{nd.lo, nd.hi, nd.size, 0};
+        } else if (act == 1) {
+            ld = leaf_desc<MC>(nd.lo, nd.hi, nd.size, p);
+            if (ld.count == 0) act = 0;
+        }
+        // leaves
+        const u32 pos = block_reserve(&p.counters[24], act == 1 ? 1u : 0u, slots);
+        bool stored = false;
+        if (act == 1) {
+            if (pos >= p.leaf_cap || ld.count > 0xffffffffull) {
                 atomicOr(&p.counters[25], 1u);
-                continue;
+            } else {
+                p.leaves[pos] = Leaf{ld.b0_lo, ld.b0_hi, ld.g0, (u32)ld.count};
+                stored = true;
             }
-            u64 m_lo = nd.lo, m_hi = nd.hi;
-            add_u128(m_lo, m_hi, half);
-            qout[pos] = MsdNode{nd.lo, nd.hi, half, level + 1, 0u};
-            qout[pos + 1] = MsdNode{m_lo, m_hi, nd.size - half, level + 1, 0u};
         }
+        if (stored) {
+            n_st++;
+            c_st += ld.count;
+            s_st += nd.size;
+        }
+        // children
+        const u32 cpos = block_reserve(&p.counters[level + 1], act == 2 ? 2u : 0u, slots);
+        if (act == 2) {
+            if (cpos + 1 >= p.q_cap) {
+                atomicOr(&p.counters[25], 1u);
+            } else {
+                const u64 half = nd.size / 2;
+                u64 m_lo = nd.lo, m_hi = nd.hi;
+                add_u128(m_lo, m_hi, half);
+                qout[cpos] = MsdNode{nd.lo, nd.hi, half, level + 1, 0u};
+                qout[cpos + 1] = MsdNode{m_lo, m_hi, nd.size - half, level + 1, 0u};
+            }
+        }
+    }
+    n_st = wave_sum(n_st);
+    c_st = wave_sum(c_st);
+    s_st = wave_sum(s_st);
+    __syncthreads();
+    if (lane == 0 && n_st) {
+        atomicAdd(&stat[0], (unsigned long long)n_st);
+        atomicAdd(&stat[1], (unsigned long long)c_st);
+        atomicAdd(&stat[2], (unsigned long long)s_st);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && stat[0]) {
+        atomicAdd(&p.counters[26], (u32)stat[0]);
+        atomicAdd((unsigned long long *)(p.counters + 28), stat[1]);
+        atomicAdd((unsigned long long *)(p.counters + 30), stat[2]);
     }
 }
 
@@ -297,7 +408,7 @@ msd_level_kernel(MsdLaunch p, u32 level, G g) {
 // ---------------------------------------------------------------------------
 template <class G>
 static hipError_t launch_nice(const NiceonlyLaunch &p, const G &g, int num_cus, hipStream_t s) {
-    u64 waves = p.n_leaves_dev ? (u64)num_cus * 32 : ((u64)p.n_leaves + 63) / 64;
+    u64 waves = p.n_leaves_dev ? (u64)num_cus * 32 : ((u64)p.n_leaves + 7) / 8;
     u64 grid = (waves + 3) / 4;
     const u64 cap = (u64)num_cus * 8;
     if (grid > cap) grid = cap;
@@ -327,7 +438,7 @@ hipError_t launch_niceonly(const NiceonlyLaunch &p, int num_cus, hipStream_t s) 
     }
 }
 
-template <class G>
+template <class G, u32 MC = 0>
 static hipError_t launch_msd(const MsdLaunch &p, const G &g, int num_cus, hipStream_t s) {
     hipLaunchKernelGGL(msd_init_kernel, dim3(256), dim3(256), 0, s, p);
     const u64 nchunks = (p.batch_size + p.chunk - 1) / p.chunk;
@@ -342,17 +453,21 @@ static hipError_t launch_msd(const MsdLaunch &p, const G &g, int num_cus, hipStr
     for (u32 level = 0; level <= last; level++) {
         const u64 nodes = level < 40 ? nchunks << level : ~0ull;
         u64 grid = (nodes + 255) / 256;
-        const u64 cap = (u64)num_cus * 8;
+        const u64 cap = (u64)num_cus * 2;
         if (grid > cap || nodes >> level != nchunks) grid = cap;
-        hipLaunchKernelGGL((msd_level_kernel<G>), dim3((u32)grid), dim3(256), 0, s, p, level, g);
+        hipLaunchKernelGGL((msd_level_kernel<G, MC>), dim3((u32)grid), dim3(256), 0, s, p, level, g);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s) {
     switch (p.base) {
-    case 40: return launch_msd(p, ConstBase<40>{}, num_cus, s);
-    case 50: return launch_msd(p, ConstBase<50>{}, num_cus, s);
+    case 40:
+        if (p.in_range && p.M == 62400) return launch_msd<ConstBase<40>, 62400>(p, ConstBase<40>{}, num_cus, s);
+        return launch_msd(p, ConstBase<40>{}, num_cus, s);
+    case 50:
+        if (p.in_range && p.M == 122500) return launch_msd<ConstBase<50>, 122500>(p, ConstBase<50>{}, num_cus, s);
+        return launch_msd(p, ConstBase<50>{}, num_cus, s);
     case 80: return launch_msd(p, ConstBase<80>{}, num_cus, s);
     default: return launch_msd(p, make_generic(p.base), num_cus, s);
     }
