@@ -60,6 +60,7 @@ detailed_generic_kernel(u64 start_lo, u64 start_hi, u64 count, GenericBase g, u3
         }
     }
     __syncthreads();
+    hist_out += (blockIdx.x % kHistCopies) * 129;
     for (u32 b = tid; b <= g.base; b += 256) {
         u32 s = hist[0][b] + hist[1][b] + hist[2][b] + hist[3][b];
         if (s) atomicAdd((unsigned long long *)&hist_out[b], (unsigned long long)s);

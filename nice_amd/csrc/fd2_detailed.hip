@@ -489,6 +489,7 @@ __device__ __forceinline__ void fd2_body(u64 start_lo, u64 start_hi, u32 nunits,
     if constexpr ((P::PROBE & 2) != 0) atomicAdd(&outl[P::W0], probe_acc);  // mass only
     __syncthreads();
     const u32 lane = tid & 63, wave = tid >> 6;
+    hist_out += (blockIdx.x % kHistCopies) * 129;
     for (u32 row = wave; row < (u32)P::W; row += P::WG / 64) {
         u32 s = 0;
 #pragma unroll

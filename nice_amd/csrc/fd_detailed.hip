@@ -403,6 +403,7 @@ detailed_fd_kernel(u64 start_lo, u64 start_hi, u64 count, u64 chunk, u32 cutoff,
     }
     __syncthreads();
     const u32 wave = tid >> 6;
+    hist_out += (blockIdx.x % kHistCopies) * 129;
     for (u32 bin = wave; bin < (u32)P::NBINS; bin += P::WG / 64) {
         u32 s = 0;
         if constexpr (P::HIST16) {

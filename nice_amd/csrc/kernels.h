@@ -15,12 +15,16 @@ struct NumOut {
     uint32_t cap;
 };
 
+// Detailed histograms live in kHistCopies copies of 129 u64 bins (summed by
+// the host); a workgroup flushes into copy blockIdx.x % kHistCopies.
+constexpr uint32_t kHistCopies = 64;
+
 struct DetailedLaunch {
     uint64_t start_lo, start_hi; // first n of the segment
     uint64_t count;              // numbers in the segment
     uint32_t base;
     uint32_t cutoff;             // near-miss cutoff (number_stats.rs:15-17)
-    uint64_t *hist;              // base+1 u64 bins, accumulated
+    uint64_t *hist;              // kHistCopies x 129 u64 bins, accumulated
     NumOut out;
 };
 

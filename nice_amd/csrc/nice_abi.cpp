@@ -31,7 +31,11 @@ using nice::u128;
 
 namespace {
 
-constexpr size_t kStateBytes = 129 * 8 + 2 * 4;  // per-device hist bins + list counters
+// Per-device state block: kHistCopies histograms of 129 u64 bins (kernels
+// spread their end-of-launch atomics over the copies: hundreds of workgroups
+// adding to ONE address serialise in L2), then the two list counters.
+constexpr size_t kHistCopies = nice::kHistCopies;
+constexpr size_t kStateBytes = kHistCopies * 129 * 8 + 2 * 4;
 
 thread_local std::string g_err;
 
@@ -77,7 +81,7 @@ struct Device {
     int num_cus = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_done = nullptr;
-    uint64_t *d_hist = nullptr;   // 129 bins, then d_count
+    uint64_t *d_hist = nullptr;   // kHistCopies x 129 bins, then d_count
     uint32_t *d_count = nullptr;  // list counters [0] detailed, [1] niceonly (inside d_hist's block)
     uint64_t *d_list_n = nullptr;
     uint32_t *d_list_u = nullptr;
@@ -174,9 +178,9 @@ int device_init(Device &d, int id) {
     HIPCHK(hipEventCreateWithFlags(&d.ev_done, hipEventDisableTiming));
     // hist bins and list counters in one block: one memset and one copy per field.
     HIPCHK(hipMalloc(&d.d_hist, kStateBytes));
-    d.d_count = (uint32_t *)(d.d_hist + 129);
+    d.d_count = (uint32_t *)(d.d_hist + kHistCopies * 129);
     HIPCHK(hipHostMalloc(&d.h_hist, kStateBytes, hipHostMallocDefault));
-    d.h_count = (uint32_t *)(d.h_hist + 129);
+    d.h_count = (uint32_t *)(d.h_hist + kHistCopies * 129);
     int rc = ensure_list(d, kInitialListCap);
     if (rc) return rc;
     return NICE_OK;
@@ -403,7 +407,8 @@ int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start
             cnt = d.h_count[0];
             if (cnt > d.list_cap) return fail(NICE_ERR_HIP, "near-miss list overflow after resize");
         }
-        for (uint32_t b = 0; b <= base; b++) total[b] += d.h_hist[b];
+        for (size_t c = 0; c < kHistCopies; c++)
+            for (uint32_t b = 0; b <= base; b++) total[b] += d.h_hist[c * 129 + b];
         if (cnt) {
             std::vector<uint64_t> nbuf((size_t)cnt * 2);
             std::vector<uint32_t> ubuf(cnt);
