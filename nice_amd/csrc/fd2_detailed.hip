@@ -47,7 +47,7 @@ namespace fd2 {
 constexpr int log2ceil(unsigned v) { int t = 0; while ((1u << t) < v) t++; return t; }
 constexpr int ilog2(unsigned v) { int t = 0; while ((2u << t) <= v) t++; return t; }
 
-template <int BASE_, int ND_, int NE_, int NE2_, int PROBE_ = 0>
+template <int BASE_, int ND_, int NE_, int NE2_, int PROBE_ = 0, int WG_ = 512>
 struct Cfg {
     static constexpr int BASE = BASE_;
     // Bottleneck probes (timing experiments only, results are wrong): 1 = no
@@ -69,7 +69,7 @@ struct Cfg {
     static constexpr int ES = MW == 1 ? 4 : (MW == 2 ? 8 : 16);  // table entry bytes
     static constexpr int SH = T + ilog2(ES);                     // carry bit of a scaled limb
     static constexpr u32 ESB = ES * B, EBT = ES * BT;
-    static constexpr int WG = 512;
+    static constexpr int WG = WG_;
     static constexpr int NBINS = BASE + 1;
     // Histogram window [W0, W0 + W): per-thread counters (u32, or u16 halves
     // shared by threads t and t + WG/2 when LDS is tight).
@@ -103,7 +103,7 @@ struct Cfg {
     static constexpr int FC = F0 + 4;  // 6-bit field: ES * (carry out of C limb 0)
     // Waves per SIMD the LDS allows (the VGPR budget is set to match).
     static constexpr int WPE0 = (163840 / LDS_BYTES) * (WG / 64) / 4;
-    static constexpr int WPE = WPE0 > 6 ? 6 : WPE0;
+    static constexpr int WPE = WPE0 > 8 ? 8 : WPE0;
     static_assert(SL < NS && CL < NC && EL <= NE, "FD layout needs cached high limbs");
     static_assert(ND <= NX + 1 && NE2 <= NX + 1 && NE <= NS + 1, "difference limb counts");
     static_assert(S_TOPD >= 1 && C_TOPD >= 1, "top limb");
@@ -508,13 +508,13 @@ __device__ __forceinline__ void fd2_body(u64 start_lo, u64 start_hi, u32 nunits,
 // Main launch: units of `chunk` numbers.  Tail launch: the < chunk numbers
 // left over, one per lane (its own symbol, so profiles show it apart).
 template <class P>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P::WPE, P::WPE)))
+__global__ void __launch_bounds__(P::WG) __attribute__((amdgpu_waves_per_eu(P::WPE, P::WPE)))
 fd2_kernel(u64 start_lo, u64 start_hi, u32 nunits, u32 chunk, u32 cutoff, u64 *__restrict__ hist_out,
            NumOut out) {
     fd2_body<P>(start_lo, start_hi, nunits, chunk, cutoff, hist_out, out);
 }
 template <class P>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(P::WPE, P::WPE)))
+__global__ void __launch_bounds__(P::WG) __attribute__((amdgpu_waves_per_eu(P::WPE, P::WPE)))
 fd2_tail_kernel(u64 start_lo, u64 start_hi, u32 nunits, u32 cutoff, u64 *__restrict__ hist_out,
                 NumOut out) {
     fd2_body<P>(start_lo, start_hi, nunits, 1u, cutoff, hist_out, out);
@@ -669,6 +669,10 @@ static hipError_t launch_segment(const DetailedLaunch &p, int num_cus, hipStream
         if (probe == 1) return launch_cfg<Cfg<40, 4, 8, 5, 1>>(p, num_cus, s);
         if (probe == 2) return launch_cfg<Cfg<40, 4, 8, 5, 2>>(p, num_cus, s);
         if (probe == 3) return launch_cfg<Cfg<40, 4, 8, 5, 3>>(p, num_cus, s);
+        // Workgroup-size sweep (profiles/r01/fd2_wg_sweep.log): 512 and 768
+        // (6 waves/SIMD) tie at 2.56-2.58 ms, 1024 (8 waves, spills) 2.59,
+        // 896 (7 waves) 2.85-2.92, 640 (5 waves) 3.18.
+        if (probe == 6) return launch_cfg<Cfg<40, 4, 8, 5, 0, 768>>(p, num_cus, s);
     }
 #define X(B_, ND_, NE_, NE2_)                                              \
     if (p.base == B_ && c.nd == ND_ && c.ne == NE_ && c.ne2 == NE2_)        \

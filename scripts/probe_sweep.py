@@ -9,7 +9,7 @@ import nice_amd as N  # noqa: E402
 
 ctx = N.GpuContext(0)
 s = N.get_base_range_u128(40).range_start
-for probe in (0, 1, 2, 3, 0):
+for probe in (0, 1, 2, 3, 6, 0):
     os.environ["NICE_FD2_PROBE"] = str(probe)
     ctx.detailed_raw(s, s + 10 ** 9, 40)
     ts = []
