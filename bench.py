@@ -67,13 +67,16 @@ def rank_field(base_start: int, rank: int):
     return start, start + FIELD_SIZE
 
 
-def timed(step, steps: int, sync, dist=None):
-    """Barrier + device sync on both sides of exactly `steps` steps; returns the
+def timed(step, steps: int, sync, dist=None, tail=None):
+    """Barrier + device sync on both sides of exactly `steps` steps (plus
+    `tail`, e.g. collecting the last step's overlapped exchange); returns the
     max elapsed seconds over ranks (all_reduce MAX)."""
     sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    if tail is not None:
+        tail()
     sync()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -127,7 +130,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    # Any torchrun launch (WORLD_SIZE set, even 1) takes the distributed path:
+    # one RCCL communicator, histogram all-reduce + list all-gather per step.
+    if "WORLD_SIZE" in os.environ:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -153,9 +158,29 @@ def main():
     last_nice_stats = None
     from nice_amd import dist as D
     whole = N.FieldSize(br.range_start, br.range_start + world * FIELD_SIZE)
+    ex = D.PipelinedExchange(dist) if dist is not None else None
+
+    def check_both(done):
+        nonlocal last_nice_stats
+        if done is None:
+            return
+        det, _, st = done
+        last_nice_stats = st or last_nice_stats
+        assert sum(d.count for d in det.distribution) == FIELD_SIZE * world
 
     def step():
         nonlocal last_nice_stats
+        if dist is not None and args.mode == "both":
+            # both modes of the rank's shard, then ONE all-reduce, overlapped
+            # with the next step's compute (nice_amd/dist.py PipelinedExchange);
+            # the previous step's results come back here and are checked.
+            t = time.perf_counter()
+            done = D.process_field_both_pipelined(ex, whole, BASE, ctx, msd_floor=args.msd_floor,
+                                                  msd_where=args.msd_where)
+            det_ms.append((time.perf_counter() - t) * 1e3)
+            kern_ms.append(ctx.kernel_stats().kernel_ms)
+            check_both(done)
+            return
         if args.mode in ("both", "detailed"):
             t = time.perf_counter()
             if dist is None:
@@ -183,10 +208,16 @@ def main():
             nice_ms.append((time.perf_counter() - t) * 1e3)
             last_nice_stats = st
 
+    def drain():
+        if ex is not None:
+            check_both(D.finish_both(ex, ex.drain()))
+
     for _ in range(args.warmup):
         step()
+    drain()
     det_ms.clear(), nice_ms.clear(), kern_ms.clear()
-    elapsed = timed(step, args.steps, barrier_sync, dist)
+
+    elapsed = timed(step, args.steps, barrier_sync, dist, tail=drain)
 
     modes = 2 if args.mode == "both" else 1
     total_numbers = modes * FIELD_SIZE * world * args.steps
@@ -221,11 +252,13 @@ def main():
             "parallelism": f"weak{world}",
         },
     }
-    if det_ms:
+    if dist is not None and args.mode == "both":
+        line["rank_step_ms"] = sum(det_ms) / len(det_ms)  # both modes + exchange, rank 0
+        det_ms.clear()  # not split per mode on this path
+        line["detailed_kernel_ms"] = sum(kern_ms) / len(kern_ms)
+    if kern_ms:
         kms = sum(kern_ms) / len(kern_ms)
         achieved = W_ALG * FIELD_SIZE / (kms / 1e3) / 1e12
-        line["detailed_numbers_per_sec"] = FIELD_SIZE / (sum(det_ms) / len(det_ms) / 1e3)
-        line["detailed_ms"] = sum(det_ms) / len(det_ms)
         line["roofline"] = {
             "bound": "valu", "kernel": "nice::fd2::fd2_kernel<Cfg<40, 4, 8, 5>>",
             "achieved": achieved, "peak": PEAK_INT32_TOPS, "unit": "int32 Tops/s",
@@ -237,10 +270,14 @@ def main():
                     "HBM bytes per launch from the committed PMC pass (profiles/r01/traffic.json, "
                     "FETCH_SIZE x2 + WRITE_SIZE), the field's bounds are the only input",
         }
+    if det_ms:
+        line["detailed_numbers_per_sec"] = FIELD_SIZE / (sum(det_ms) / len(det_ms) / 1e3)
+        line["detailed_ms"] = sum(det_ms) / len(det_ms)
     if nice_ms:
         line["niceonly_numbers_per_sec"] = FIELD_SIZE / (sum(nice_ms) / len(nice_ms) / 1e3)
         line["niceonly_ms"] = sum(nice_ms) / len(nice_ms)
-        st = last_nice_stats
+    st = last_nice_stats
+    if st is not None and (nice_ms or dist is not None):
         line["niceonly"] = {"ranges": st.ranges, "range_numbers": st.range_numbers,
                             "candidates": st.candidates, "launches": st.launches,
                             "msd_seconds": st.msd_seconds, "total_seconds": st.total_seconds}

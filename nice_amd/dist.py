@@ -5,12 +5,13 @@ the 8 GPUs of one node; the tiny histograms are combined with an RCCL
 all-reduce over xGMI, and nice-number lists are gathered to the host."
 
 One process per GPU.  Rank r takes the r-th contiguous shard of [start, end)
-and runs the library on its own device; the only exchange is
-
-  detailed:  all_reduce(SUM) of the (base + 1)-bin u64 histogram, then an
-             all_gather of the near-miss lists (count first, then the padded
-             (lo, hi, num_uniques) rows);
-  niceonly:  the same all_gather of the nice lists.
+and runs the library on its own device; the only exchange is ONE all-reduce
+(SUM, int64) of [the (base + 1)-bin histogram, every rank's list length] —
+a rank writes its own length into its slot of a one-hot block — followed by
+an all-gather of the padded (lo, hi, num_uniques) rows only when some list is
+non-empty (near-misses and nice numbers are rare: usually no second
+collective).  `process_field_both_dist` does detailed and niceonly of a field
+with that single all-reduce.
 
 Shards are contiguous and ordered by rank, so concatenating the gathered lists
 in rank order is already ascending (the reference sorts after the fact,
@@ -60,15 +61,31 @@ def _to_i64(v: int) -> int:
     return v - (1 << 64) if v >> 63 else v
 
 
-def _gather_rows(rows: Sequence[Tuple[int, int]], dist, group) -> List[Tuple[int, int]]:
-    """all_gather of variable-length (number, aux) lists, in rank order."""
+def _all_reduce_ints(vals: Sequence[int], dist, group) -> List[int]:
+    """One SUM all-reduce of an int64 vector (one H2D, one collective, one D2H)."""
+    import torch
+    t = torch.tensor(list(vals), dtype=torch.int64).to(_device(dist, group))
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t.cpu().tolist()
+
+
+def _onehot(rank: int, world: int, v: int) -> List[int]:
+    out = [0] * world
+    out[rank] = v
+    return out
+
+
+def _gather_rows(rows: Sequence[Tuple[int, int]], dist, group,
+                 counts: Optional[Sequence[int]] = None) -> List[Tuple[int, int]]:
+    """all_gather of variable-length (number, aux) lists, in rank order.  With
+    `counts` (every rank's list length, already exchanged) no count collective
+    is issued, and nothing at all when every list is empty."""
     import torch
     dev = _device(dist, group)
     world = dist.get_world_size(group)
-    cnt = torch.tensor([len(rows)], dtype=torch.int64, device=dev)
-    counts = [torch.zeros_like(cnt) for _ in range(world)]
-    dist.all_gather(counts, cnt, group=group)
-    counts = [int(c.item()) for c in counts]
+    if counts is None:
+        counts = _all_reduce_ints(_onehot(dist.get_rank(group), world, len(rows)), dist, group)
+    counts = [int(c) for c in counts]
     width = max(counts)
     if width == 0:
         return []
@@ -90,21 +107,147 @@ def _gather_rows(rows: Sequence[Tuple[int, int]], dist, group) -> List[Tuple[int
 def process_range_detailed_dist(range_: FieldSize, base: int, ctx=None, group=None,
                                 shard_fn: Optional[Callable] = None) -> FieldResults:
     """process_range_detailed over a process group: every rank returns the
-    whole field's FieldResults (identical to the single-process result)."""
-    import torch
+    whole field's FieldResults (identical to the single-process result).  One
+    all-reduce carries the histogram and every rank's near-miss count; the
+    lists are all-gathered only when some rank has entries."""
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     s, e = shard_bounds(range_.range_start, range_.range_end, rank, world)
     if shard_fn is None:
         shard_fn = ctx.detailed_raw
     hist, lst = shard_fn(s, e, base)
-    h = torch.tensor(list(hist[: base + 1]), dtype=torch.int64, device=_device(dist, group))
-    dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
-    hist = [int(x) for x in h.cpu().tolist()]
-    rows = _gather_rows(lst, dist, group)
+    red = _all_reduce_ints(list(hist[: base + 1]) + _onehot(rank, world, len(lst)), dist, group)
+    hist, counts = red[: base + 1], red[base + 1:]
+    rows = _gather_rows(lst, dist, group, counts=counts)
     return FieldResults(
         distribution=[UniquesDistributionSimple(i, hist[i]) for i in range(1, base + 1)],
         nice_numbers=[NiceNumberSimple(n, u) for n, u in rows])
+
+
+def niceonly_shard_bounds(range_: FieldSize, rank: int, world: int, chunk: int = 0):
+    """Rank r's niceonly shard: cut on the whole field's client chunk grid."""
+    chunk = chunk or client_chunk_size(range_.range_size)
+    s, e = shard_bounds(range_.range_start, range_.range_end, rank, world, grain=chunk)
+    return s, e, chunk
+
+
+def process_field_both_dist(range_: FieldSize, base: int, ctx, group=None,
+                            **nice_opts):
+    """Detailed AND niceonly of one field over a process group with ONE
+    exchange: a single all-reduce of [histogram, near-miss counts per rank,
+    nice counts per rank]; the lists are all-gathered only if non-empty.
+    Returns (detailed FieldResults, niceonly FieldResults, this rank's
+    niceonly statistics or None)."""
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    s, e = shard_bounds(range_.range_start, range_.range_end, rank, world)
+    hist, near = ctx.detailed_raw(s, e, base)
+    ns, ne, chunk = niceonly_shard_bounds(range_, rank, world, nice_opts.pop("chunk_size", 0))
+    nice, stats = ctx.niceonly_raw(ns, ne, base, chunk_size=chunk, **nice_opts) if ns < ne \
+        else ([], None)
+    red = _all_reduce_ints(list(hist[: base + 1]) + _onehot(rank, world, len(near))
+                           + _onehot(rank, world, len(nice)), dist, group)
+    hist = red[: base + 1]
+    near_rows = _gather_rows(near, dist, group, counts=red[base + 1: base + 1 + world])
+    nice_rows = _gather_rows([(n, base) for n in nice], dist, group,
+                             counts=red[base + 1 + world:])
+    det = FieldResults(
+        distribution=[UniquesDistributionSimple(i, hist[i]) for i in range(1, base + 1)],
+        nice_numbers=[NiceNumberSimple(n, u) for n, u in near_rows])
+    return det, FieldResults(distribution=[],
+                             nice_numbers=[NiceNumberSimple(n, u) for n, u in nice_rows]), stats
+
+
+class PipelinedExchange:
+    """Overlap each field's exchange with the next field's compute: submit()
+    starts the all-reduce of this field's [histogram, counts] vector
+    asynchronously (RCCL runs it while the ranks process the next field) and
+    returns the PREVIOUS field's reduced vector; drain() returns the last one.
+    The lists of a field are gathered when its vector is collected (only if
+    non-empty, which is rare).  Two preallocated device vectors alternate, fed
+    from / read back into pinned host memory, so a step costs one async copy
+    each way and one collective launch."""
+
+    def __init__(self, dist, group=None, width: int = 0):
+        self.dist, self.group = dist, group
+        self.pending = None
+        self.width = 0
+        self.bufs = []
+        self.flip = 0
+        if width:
+            self._alloc(width)
+
+    def _alloc(self, width: int):
+        import torch
+        dev = _device(self.dist, self.group)
+        pin = dev.type == "cuda"
+        self.bufs = [(torch.zeros(width, dtype=torch.int64, pin_memory=pin),
+                      torch.zeros(width, dtype=torch.int64, device=dev),
+                      torch.zeros(width, dtype=torch.int64, pin_memory=pin)) for _ in range(2)]
+        self.width = width
+
+    def submit(self, vals: Sequence[int], payload):
+        if len(vals) != self.width:
+            self.drain_check()
+            self._alloc(len(vals))
+        h_in, d, h_out = self.bufs[self.flip]
+        self.flip ^= 1
+        h_in.numpy()[:] = vals
+        d.copy_(h_in, non_blocking=True)
+        work = self.dist.all_reduce(d, op=self.dist.ReduceOp.SUM, group=self.group, async_op=True)
+        prev, self.pending = self.pending, (work, d, h_out, payload)
+        return self._collect(prev)
+
+    def drain_check(self):
+        if self.pending is not None:
+            raise RuntimeError("PipelinedExchange: drain() before changing the vector width")
+
+    def drain(self):
+        prev, self.pending = self.pending, None
+        return self._collect(prev)
+
+    def _collect(self, p):
+        if p is None:
+            return None
+        work, d, h_out, payload = p
+        work.wait()
+        h_out.copy_(d)  # synchronises with the collective's stream
+        return h_out.tolist(), payload
+
+
+def process_field_both_pipelined(ex: PipelinedExchange, range_: FieldSize, base: int, ctx,
+                                 **nice_opts):
+    """process_field_both_dist with the exchange overlapped (see
+    PipelinedExchange): computes this rank's shards of `range_`, starts their
+    exchange, and returns the PREVIOUS submitted field's (detailed, niceonly,
+    stats) results (None on the first call); ex.drain() + finish_both() give
+    the last field's."""
+    dist, group = ex.dist, ex.group
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    s, e = shard_bounds(range_.range_start, range_.range_end, rank, world)
+    hist, near = ctx.detailed_raw(s, e, base)
+    ns, ne, chunk = niceonly_shard_bounds(range_, rank, world, nice_opts.pop("chunk_size", 0))
+    nice, stats = ctx.niceonly_raw(ns, ne, base, chunk_size=chunk, **nice_opts) if ns < ne \
+        else ([], None)
+    vec = list(hist[: base + 1]) + _onehot(rank, world, len(near)) + _onehot(rank, world, len(nice))
+    return finish_both(ex, ex.submit(vec, (base, near, nice, stats)))
+
+
+def finish_both(ex: PipelinedExchange, collected):
+    """Turn a collected (vector, payload) pair into (detailed, niceonly, stats)."""
+    if collected is None:
+        return None
+    red, (base, near, nice, stats) = collected
+    world = ex.dist.get_world_size(ex.group)
+    hist = red[: base + 1]
+    near_rows = _gather_rows(near, ex.dist, ex.group, counts=red[base + 1: base + 1 + world])
+    nice_rows = _gather_rows([(n, base) for n in nice], ex.dist, ex.group,
+                             counts=red[base + 1 + world:])
+    det = FieldResults(
+        distribution=[UniquesDistributionSimple(i, hist[i]) for i in range(1, base + 1)],
+        nice_numbers=[NiceNumberSimple(n, u) for n, u in near_rows])
+    return det, FieldResults(distribution=[],
+                             nice_numbers=[NiceNumberSimple(n, u) for n, u in nice_rows]), stats
 
 
 def process_range_niceonly_dist(range_: FieldSize, base: int, ctx=None, group=None,
@@ -113,8 +256,7 @@ def process_range_niceonly_dist(range_: FieldSize, base: int, ctx=None, group=No
     field's client chunk grid, see module doc)."""
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    chunk = opts.pop("chunk_size", 0) or client_chunk_size(range_.range_size)
-    s, e = shard_bounds(range_.range_start, range_.range_end, rank, world, grain=chunk)
+    s, e, chunk = niceonly_shard_bounds(range_, rank, world, opts.pop("chunk_size", 0))
     if s < e:
         if shard_fn is None:
             lst, _ = ctx.niceonly_raw(s, e, base, chunk_size=chunk, **opts)

@@ -69,6 +69,16 @@ def _oracle_niceonly_shard(s, e, base, chunk):
     return out
 
 
+class _OracleCtx:
+    """Stands in for nice_amd.GpuContext in the CPU tests (oracle-backed)."""
+
+    def detailed_raw(self, s, e, base):
+        return _oracle_detailed_shard(s, e, base)
+
+    def niceonly_raw(self, s, e, base, chunk_size=0, **_):
+        return _oracle_niceonly_shard(s, e, base, chunk_size), None
+
+
 def _field_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -86,6 +96,21 @@ def _field_worker(rank, world, port, q):
     r = D.process_range_niceonly_dist(FieldSize(s40, s40 + 10 ** 6), 40, chunk_size=99_991,
                                       shard_fn=_oracle_niceonly_shard)
     res["nice_b40"] = [(n.number, n.num_uniques) for n in r.nice_numbers]
+    # both modes with one exchange (bench.py's N > 1 step), oracle-backed context
+    det, nic, _ = D.process_field_both_dist(FieldSize(10 ** 6 - 53, 10 ** 6 + 3_000), 10,
+                                            _OracleCtx(), chunk_size=1_013)
+    res["both_b10"] = ([(d.num_uniques, d.count) for d in det.distribution],
+                       [(n.number, n.num_uniques) for n in det.nice_numbers],
+                       [n.number for n in nic.nice_numbers])
+    # the pipelined exchange returns each field's results one call later
+    ex = D.PipelinedExchange(dist)
+    fields = [FieldSize(a, a + 2_000) for a in (47, 10 ** 6 - 53, 2 * 10 ** 6)]
+    got = [D.process_field_both_pipelined(ex, f, 10, _OracleCtx(), chunk_size=997) for f in fields]
+    got.append(D.finish_both(ex, ex.drain()))
+    assert got[0] is None
+    res["pipelined"] = [([(d.num_uniques, d.count) for d in r[0].distribution],
+                         [(n.number, n.num_uniques) for n in r[0].nice_numbers],
+                         [n.number for n in r[1].nice_numbers]) for r in got[1:]]
     q.put((rank, res))
     dist.destroy_process_group()
 
@@ -112,6 +137,14 @@ def test_two_rank_field_sharding_matches_single_process():
     assert len(w.nice_numbers) == 5395  # lists gathered in ascending order
     assert out[0]["nice_b10"] == [(69, 10)]
     assert out[0]["nice_b40"] == []
+    w = O.process_range_detailed(10 ** 6 - 53, 10 ** 6 + 3_000, 10)
+    want_nice = _oracle_niceonly_shard(10 ** 6 - 53, 10 ** 6 + 3_000, 10, 1_013)
+    assert out[0]["both_b10"] == (w.distribution, w.nice_numbers, want_nice)
+    assert len(w.nice_numbers) > 1000
+    for (a, r) in zip((47, 10 ** 6 - 53, 2 * 10 ** 6), out[0]["pipelined"]):
+        w = O.process_range_detailed(a, a + 2_000, 10)
+        assert r == (w.distribution, w.nice_numbers, _oracle_niceonly_shard(a, a + 2_000, 10, 997))
+    assert out[0]["pipelined"][0][2] == [69]
     # shard cuts fall on the whole field's chunk grid
     assert D.shard_bounds(0, 10 ** 6, 0, 2, 99_991)[1] % 99_991 == 0
     assert D.shard_bounds(0, 10, 1, 3) == (4, 7)
