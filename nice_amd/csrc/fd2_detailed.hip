@@ -9,14 +9,18 @@
 //
 //  * Each lane walks a contiguous chunk n0 .. n0+len-1 (len <= B = b^2).
 //    n^2 and n^3 live in radix-B limbs (one limb = two base-b digits) and step
-//    by finite differences, never multiplying or dividing:
-//        S = n^2 += D1,  D1 = 2n + 1        += 2
-//        C = n^3 += E1,  E1 = 3n^2 + 3n + 1 += E2,  E2 = 6n + 6 += 6
+//    by finite differences, never dividing:
+//        S = n^2 += D1,            D1 = 2n + 1 += 2
+//        C = n^3 += 3 S + N3,      N3 = 3n + 1 += 3
+//    (the cube's increment 3n^2 + 3n + 1 is rebuilt from the square's limbs,
+//    so no second-order difference state is carried).  A C-limb sum is < 5B:
+//    its carry (0..4) is one multiply-high (two for b80).
 //  * Limb counts are template parameters picked by the host per segment
-//    (ND, NE, NE2 = limbs of D1, E1, E2 at the segment's end), so a step adds
-//    exactly the limbs that can change: S limbs [0, ND], C limbs [0, NE], E1
-//    limbs [0, NE2].  Carries out of those (probability ~1/B per step) and the
-//    limb-0 wraps of D1 / E2 take a rare, wave-uniform branch.
+//    (ND, NE = limbs of D1 = 2e+1 and E1 = 3e^2+3e+1 at the segment's end,
+//    NE2 of 6e+6 kept for the layout checks), so a step touches exactly the
+//    limbs that can change: S limbs [0, ND], C limbs [0, NE].  Carries out of
+//    those (probability ~1/B per step) and the limb-0 wraps of D1 / N3 take a
+//    rare, wave-uniform branch.
 //  * The per-step limbs are stored SCALED by the mask-table entry size ES and
 //    BIASED by 2^T - B: the stored word is directly the LDS byte address of the
 //    limb's digit-pair mask (no address arithmetic), and the radix-B carry is
@@ -85,21 +89,26 @@ struct Cfg {
     static constexpr int LDS_BYTES = TL + (LSD ? (int)(2 * B * ES) : 0);
     static constexpr int LO = LSD ? 1 : 0;  // first stored / looked-up limb
     // Low-digit entry, word 1: digit bits [0, DB), then flags and carries of
-    // the step n -> n+1, all functions of n mod B (limb 0 of S, C, D1, E1, E2
-    // is never stored): bit DB: D1 limb-0 wrap, DB+1: E2 limb-0 wrap; 4-bit
-    // fields at F0, F0+4, F0+8 hold 8 * (carry out of limb 0) of S += D1,
-    // C += E1, E1 += E2 (ES = 8, so a field IS the scaled carry).
+    // the step n -> n+1, all functions of n mod B (limb 0 of S, C, D1, N3
+    // is never stored): bit DB: D1 limb-0 wrap, DB+1: N3 limb-0 wrap; a 4-bit
+    // field at F0 holds 8 * (carry out of S limb 0) of S += D1 and a 6-bit
+    // field at FC = F0+4 holds 8 * (carry 0..4 out of C limb 0) of
+    // C += 3S + N3 (ES = 8, so a field IS the scaled carry).
     static constexpr int DB = BASE - 32;
     static constexpr u32 DMASK = (1u << (DB > 0 ? DB : 0)) - 1;
     static constexpr u32 FLAGS = 3u << DB;
     static constexpr int F0 = (DB + 2 + 3) / 4 * 4;
-    // LSD bases step C by C += 3S + N3 (N3 = 3n + 1, NN limbs): no E1 / E2
-    // state.  A C limb sum is < 5B, so its carry (0..4) is a multiply-high
-    // by MAGIC = ceil(2^32 / (ES B)) (exact over the range: static_assert).
+    // C += 3S + N3 (N3 = 3n + 1, NN limbs).  A C limb sum is < 5B, so its
+    // carry (0..4) is a multiply-high by MAGIC = ceil(2^32 / (ES B)) (exact
+    // over the range: static_assert).
     static constexpr int NN = NX + 1;
     static constexpr u32 DC = ES * B;
     static constexpr u32 MAGIC = (u32)(((1ull << 32) + DC - 1) / DC);
     static constexpr unsigned long long TMAX = (unsigned long long)ES * (5ull * B + 4);
+    // Where one multiply-high by ceil(2^32 / (ES B)) is not exact over
+    // [0, TMAX] (b80: ES = 16), divide t / ES first (t is a multiple of ES).
+    static constexpr bool C1 = ((unsigned long long)MAGIC * DC - (1ull << 32)) * TMAX < (1ull << 32);
+    static constexpr u32 MAGICB = (u32)(((1ull << 32) + B - 1) / B);
     static constexpr int FC = F0 + 4;  // 6-bit field: ES * (carry out of C limb 0)
     // Waves per SIMD the LDS allows (the VGPR budget is set to match).
     static constexpr int WPE0 = (163840 / LDS_BYTES) * (WG / 64) / 4;
@@ -111,9 +120,10 @@ struct Cfg {
     static_assert(LDS_BYTES <= 163840, "LDS");
     static_assert(W0 + W <= NBINS, "window");
     static_assert(!LSD || (ES == 8 && DB > 0 && FC + 6 <= 32), "low-digit entry layout");
-    static_assert(!LSD || ((unsigned long long)MAGIC * DC - (1ull << 32)) * TMAX < (1ull << 32),
+    static_assert(C1 || ((unsigned long long)MAGICB * B - (1ull << 32)) * (TMAX / ES) < (1ull << 32),
                   "C-limb carry magic");
-    static_assert(!LSD || (NN <= SL && NE >= NS), "C += 3S + N3 layout");
+    static_assert(NN <= SL && NE >= NS, "C += 3S + N3 layout");
+    static_assert(3 * ES <= 64, "inline-constant multiplier");
 };
 
 // v_mad_u32_u24 with an inline-constant multiplier (LLVM otherwise splits it
@@ -131,9 +141,7 @@ struct State {
     u32 S[P::NS];    // n^2: limbs [0, SL) scaled+biased, [SL, NS) plain
     u32 C[P::NC];    // n^3: same with CL
     u32 D1[P::ND];   // scaled, plain
-    u32 E1[P::NE];   // scaled, plain
-    u32 E2[P::NE2];  // scaled, plain (non-LSD bases)
-    u32 N3[P::NN];   // LSD bases: 3n + 1, scaled, limb i < SL offset by -3 ES BT
+    u32 N3[P::NN];   // 3n + 1, scaled, limb i < SL offset by -3 ES BT
     u32 r8;          // low-digit table byte offset: ES * (n mod B + i)
     u32 hi[P::MW];   // mask of the cached (rarely changing) limbs of S and C
 };
@@ -230,37 +238,20 @@ __device__ __forceinline__ void init(State<P> &st, u64 n_lo, u64 n_hi, const uns
         for (int t = 0; t < P::NX; t++) acc[t] = 2ull * X[t] + (t == 0 ? 1 : 0);
         normalize<P>(acc, st.D1);
     }
-    {  // E1 = 3n^2 + 3n + 1
-        u64 acc[P::NS];
-#pragma unroll
-        for (int t = 0; t < P::NS; t++)
-            acc[t] = 3ull * st.S[t] + (t < P::NX ? 3ull * X[t] : 0) + (t == 0 ? 1 : 0);
-        normalize<P>(acc, st.E1);
-    }
     {  // N3 = 3n + 1
         u64 acc[P::NX];
 #pragma unroll
         for (int t = 0; t < P::NX; t++) acc[t] = 3ull * X[t] + (t == 0 ? 1 : 0);
         normalize<P>(acc, st.N3);
     }
-    {  // E2 = 6n + 6
-        u64 acc[P::NX];
-#pragma unroll
-        for (int t = 0; t < P::NX; t++) acc[t] = 6ull * X[t] + (t == 0 ? 6 : 0);
-        normalize<P>(acc, st.E2);
-    }
     recompute_hi<P>(st, smem);
     if constexpr (P::LSD) st.S[0] = st.C[0] = st.D1[0] = st.N3[0] = 0;  // from the table
 #pragma unroll
     for (int i = 0; i < P::SL; i++) st.S[i] = (st.S[i] + P::BT) * P::ES;
 #pragma unroll
-    for (int i = 0; i < P::CL; i++) st.C[i] = (st.C[i] + (P::LSD ? 0u : P::BT)) * P::ES;
+    for (int i = 0; i < P::CL; i++) st.C[i] *= P::ES;  // unbiased: carries by multiply-high
 #pragma unroll
     for (int i = 0; i < P::ND; i++) st.D1[i] *= P::ES;
-#pragma unroll
-    for (int i = 0; i < P::NE; i++) st.E1[i] *= P::ES;
-#pragma unroll
-    for (int i = 0; i < P::NE2; i++) st.E2[i] *= P::ES;
 #pragma unroll
     for (int i = 0; i < P::NN; i++) st.N3[i] = st.N3[i] * P::ES - (i < P::SL ? 3 * P::EBT : 0u);
 }
@@ -306,13 +297,9 @@ __device__ __forceinline__ void carry_n3(State<P> &st) {
 template <class P>
 __device__ __forceinline__ void rare(State<P> &st, const unsigned char *smem, u32 d1w, u32 e2w, u32 cS,
                                      u32 cC, u32 cE) {
+    (void)cE;
     if (d1w) carry_scaled<P>(st.D1, 1);
-    if constexpr (P::LSD) {
-        if (e2w) carry_n3<P>(st);
-    } else {
-        if (e2w) carry_scaled<P>(st.E2, 1);
-        if (cE) carry_scaled<P>(st.E1, P::EL);
-    }
+    if (e2w) carry_n3<P>(st);
     if (cS) carry_plain<P>(st.S, P::SL);
     if (cC) carry_plain<P>(st.C, P::CL);
     if (cS | cC) recompute_hi<P>(st, smem);
@@ -325,61 +312,45 @@ __device__ __forceinline__ void rare(State<P> &st, const unsigned char *smem, u3
 template <class P>
 __device__ __forceinline__ void step(State<P> &st, const unsigned char *smem, u32 w1) {
     constexpr u32 ES = P::ES;
+    constexpr int L0 = P::LO;  // LSD bases: limb 0 lives in the low-digit table
+    // C += 3S + N3 (old S), limbs L0 .. CL-1.  Unbiased scaled limbs; a limb
+    // sum is < 5B, its carry (0..4) is a multiply-high.
+    u32 cC = 0;
+    if constexpr (P::LSD) cC = __builtin_amdgcn_ubfe(w1, P::FC, 6);
+#pragma unroll
+    for (int i = L0; i < P::CL; i++) {
+        u32 t = st.C[i] + cC;
+        if (i < P::NN) t += st.N3[i];
+        else if (i < P::SL) t -= 3 * P::EBT;
+        // + 3S as one v_mad_u32_u24 (limbs < 2^24)
+        if (i < P::SL) t = mad_u24<3>(st.S[i], t);
+        else if (i < P::NS) t = mad_u24<3 * ES>(st.S[i], t);
+        const u32 c = P::C1 ? __umulhi(t, P::MAGIC) : __umulhi(t / ES, P::MAGICB);
+        st.C[i] = t - c * P::DC;
+        cC = c * ES;
+    }
+    // S += D1, limbs L0 .. SL-1 (biased: carry = bit T of t >> log2 ES).
+    u32 cS = 0;
+    if constexpr (P::LSD) cS = __builtin_amdgcn_ubfe(w1, P::F0, 4);
+#pragma unroll
+    for (int i = L0; i < P::SL; i++) {
+        u32 t = st.S[i] + (i < P::ND ? st.D1[i] : 0u) + cS;
+        cS = (t >> P::T) & ES;
+        st.S[i] = t - cS * P::B;
+    }
+    st.r8 += ES;
     if constexpr (P::LSD) {
-        // C += 3S + N3 (old S), limbs 1 .. CL-1; carry into limb 1 from the table.
-        u32 cC = __builtin_amdgcn_ubfe(w1, P::FC, 6);
-#pragma unroll
-        for (int i = 1; i < P::CL; i++) {
-            u32 t = st.C[i] + cC;
-            if (i < P::NN) t += st.N3[i];
-            else if (i < P::SL) t -= 3 * P::EBT;
-            // + 3S as one v_mad_u32_u24 (limbs < 2^24)
-            if (i < P::SL) t = mad_u24<3>(st.S[i], t);
-            else if (i < P::NS) t = mad_u24<3 * ES>(st.S[i], t);
-            const u32 c = __umulhi(t, P::MAGIC);
-            st.C[i] = t - c * P::DC;
-            cC = c * ES;
-        }
-        // S += D1, limbs 1 .. SL-1 (biased: carry = bit T of t >> LG).
-        u32 cS = __builtin_amdgcn_ubfe(w1, P::F0, 4);
-#pragma unroll
-        for (int i = 1; i < P::SL; i++) {
-            u32 t = st.S[i] + (i < P::ND ? st.D1[i] : 0u) + cS;
-            cS = (t >> P::T) & ES;
-            st.S[i] = t - cS * P::B;
-        }
-        st.r8 += ES;
         if (((w1 & P::FLAGS) | cS | cC) != 0)
             rare<P>(st, smem, w1 & (1u << P::DB), w1 & (2u << P::DB), cS, cC, 0);
     } else {
-        u32 cS = 0, cC = 0, cE = 0;
-#pragma unroll
-        for (int i = 0; i < P::SL; i++) {
-            u32 t = st.S[i] + (i < P::ND ? st.D1[i] : 0u) + cS;
-            cS = (t >> P::T) & ES;
-            st.S[i] = t - cS * P::B;
-        }
-#pragma unroll
-        for (int i = 0; i < P::CL; i++) {
-            u32 t = st.C[i] + (i < P::NE ? st.E1[i] : 0u) + cC;
-            cC = (t >> P::T) & ES;
-            st.C[i] = t - cC * P::B;
-        }
-        // E1 += E2 (plain scaled: the bias is added for the carry test only).
-#pragma unroll
-        for (int i = 0; i < P::EL; i++) {
-            u32 t = st.E1[i] + (i < P::NE2 ? st.E2[i] : 0u) + cE;
-            cE = ((t + P::EBT) >> P::T) & ES;
-            st.E1[i] = t - cE * P::B;
-        }
-        st.r8 += ES;
+        // limb 0 of D1 (+2) and N3 (+3, stored offset by -3 ES BT) step here
         st.D1[0] += 2 * ES;
-        st.E2[0] += 6 * ES;
-        const u32 d1w = st.D1[0] >= P::ESB, e2w = st.E2[0] >= P::ESB;
-        if ((cS | cC | cE | d1w | e2w) != 0) {
+        st.N3[0] += 3 * ES;
+        const u32 d1w = st.D1[0] >= P::ESB, n3w = st.N3[0] + 3 * P::EBT >= P::ESB;
+        if ((cS | cC | d1w | n3w) != 0) {
             if (d1w) st.D1[0] -= P::ESB;
-            if (e2w) st.E2[0] -= P::ESB;
-            rare<P>(st, smem, d1w, e2w, cS, cC, cE);
+            if (n3w) st.N3[0] -= P::ESB;
+            rare<P>(st, smem, d1w, n3w, cS, cC, 0);
         }
     }
 }
@@ -461,7 +432,7 @@ __device__ __forceinline__ void fd2_body(u64 start_lo, u64 start_hi, u32 nunits,
                 for (int q = P::LO; q < P::SL; q++) or_entry<P>(smem + (P::TB - P::EBT) + st.S[q], m);
 #pragma unroll
                 for (int q = P::LO; q < P::CL; q++)
-                    or_entry<P>(smem + (P::LSD ? P::TB : P::TB - P::EBT) + st.C[q], m);
+                    or_entry<P>(smem + P::TB + st.C[q], m);
             }
             u32 uw = (u32)(-P::W0);
 #pragma unroll
@@ -656,6 +627,10 @@ static const BaseThresholds &thresholds(uint32_t base) {
     return t;
 }
 
+// Workgroup size per base.  b80's 102 KB mask table leaves room for one
+// workgroup per CU; 768 threads (3 waves/SIMD) would need <= 168 VGPRs and
+// spills (3.19 ms per 2e8) where 512 threads at 2 waves/SIMD do not (2.83 ms).
+#define WG_FOR(b) 512
 #define FD2_COMBOS(X)                                                                           \
     X(40, 4, 8, 5) X(40, 5, 8, 5) X(40, 5, 9, 5) X(50, 5, 10, 6) X(50, 6, 10, 6) X(50, 6, 11, 6) \
         X(80, 8, 16, 9) X(80, 9, 16, 9) X(80, 9, 17, 9)
@@ -676,7 +651,7 @@ static hipError_t launch_segment(const DetailedLaunch &p, int num_cus, hipStream
     }
 #define X(B_, ND_, NE_, NE2_)                                              \
     if (p.base == B_ && c.nd == ND_ && c.ne == NE_ && c.ne2 == NE2_)        \
-        return launch_cfg<Cfg<B_, ND_, NE_, NE2_>>(p, num_cus, s);
+        return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WG_FOR(B_)>>(p, num_cus, s);
     FD2_COMBOS(X)
 #undef X
     return hipErrorInvalidValue;

@@ -10,8 +10,11 @@ sys.path.insert(0, ROOT)
 import nice_amd as N  # noqa: E402
 
 cfg = [(40, 10 ** 9), (50, 10 ** 9), (80, 2 * 10 ** 8)]
+if os.environ.get("SWEEP_BASES"):
+    keep = {int(b) for b in os.environ["SWEEP_BASES"].split(",")}
+    cfg = [c for c in cfg if c[0] in keep]
 variants = [int(v) for v in os.environ.get("SWEEP_VARIANTS", "0,1,2,3,8,9,10,11").split(",")]
-reps = 3
+reps = int(os.environ.get("SWEEP_REPS", "3"))
 ctx = N.GpuContext(0)
 res = {}
 for base, size in cfg:
