@@ -509,19 +509,26 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
     while (left) {
         const u64 cnt = left < max_count ? left : max_count;
         // Chunks of <= B numbers (low-digit table), about 3 per lane.
+        // Chunks of <= B numbers (low-digit table), about 3 per lane, and never
+        // more units than lanes x units-per-lane: a lane with one unit more
+        // than the rest runs alone at the end (989 such units on the b40 1e9
+        // field once cost ~7 % of the launch).
         const u64 per_lane = (cnt + lanes - 1) / lanes;
-        const u64 units_per_lane = (per_lane + P::B - 1) / P::B < 3 ? 3 : (per_lane + P::B - 1) / P::B;
-        u64 chunk = (cnt + lanes * units_per_lane - 1) / (lanes * units_per_lane);
-        // A lane's init (radix-B conversion, products) costs about ten steps:
-        // small fields use fewer lanes with >= 32 numbers each instead of
-        // one number per lane.
-        if (chunk < 32) chunk = cnt < 32 ? cnt : 32;
-        if (chunk < 1) chunk = 1;
-        if (chunk > P::B) chunk = P::B;
-        // Odd chunks: lane l of a wave then sits at n mod B = r0 + chunk * l,
-        // so its low-digit entries fall on 32 distinct bank pairs per half-wave
-        // (B is a multiple of 32 for the LSD bases): conflict-free lookups.
-        if (P::LSD && chunk > 1 && chunk % 2 == 0) chunk--;
+        u64 upl = (per_lane + P::B - 1) / P::B < 3 ? 3 : (per_lane + P::B - 1) / P::B;
+        u64 chunk;
+        for (;; upl++) {
+            chunk = (cnt + lanes * upl - 1) / (lanes * upl);  // ceil: cnt / chunk <= lanes * upl
+            // A lane's init (radix-B conversion, products) costs about ten
+            // steps: small fields use fewer lanes with >= 32 numbers each.
+            if (chunk < 32) chunk = cnt < 32 ? cnt : 32;
+            if (chunk < 1) chunk = 1;
+            // Odd chunks: lane l of a wave then sits at n mod B = r0 + chunk * l,
+            // so its low-digit entries fall on 32 distinct bank pairs per
+            // half-wave (B is a multiple of 32 for the LSD bases): rounding UP
+            // keeps the unit count within lanes x upl.
+            if (P::LSD && chunk > 1 && chunk % 2 == 0) chunk++;
+            if (chunk <= P::B) break;
+        }
         u64 nunits = cnt / chunk;
         if (nunits > 0xffffffffull) return hipErrorInvalidValue;
         if (nunits) {
