@@ -88,16 +88,17 @@ struct Cfg {
     static constexpr int TL = TB + (int)(B * ES);                // low-digit table (2B entries)
     static constexpr int LDS_BYTES = TL + (LSD ? (int)(2 * B * ES) : 0);
     static constexpr int LO = LSD ? 1 : 0;  // first stored / looked-up limb
-    // Low-digit entry, word 1: digit bits [0, DB), then flags and carries of
-    // the step n -> n+1, all functions of n mod B (limb 0 of S, C, D1, N3
-    // is never stored): bit DB: D1 limb-0 wrap, DB+1: N3 limb-0 wrap; a 4-bit
-    // field at F0 holds 8 * (carry out of S limb 0) of S += D1 and a 6-bit
-    // field at FC = F0+4 holds 8 * (carry 0..4 out of C limb 0) of
-    // C += 3S + N3 (ES = 8, so a field IS the scaled carry).
+    // Low-digit entry, word 1: digit bits [0, DB), then the carries and flags
+    // of the step n -> n+1, all functions of n mod B (limb 0 of S, C, D1, N3
+    // is never stored): a 4-bit field at F0 holds 8 * (carry out of S limb 0)
+    // of S += D1 and a 6-bit field at FC = F0+4 holds 8 * (carry 0..4 out of
+    // C limb 0) of C += 3S + N3 (ES = 8, so a field IS the scaled carry);
+    // bit 30: D1 limb-0 wrap, bit 31: N3 limb-0 wrap (top bits, so "any flag"
+    // is one compare).
     static constexpr int DB = BASE - 32;
     static constexpr u32 DMASK = (1u << (DB > 0 ? DB : 0)) - 1;
-    static constexpr u32 FLAGS = 3u << DB;
-    static constexpr int F0 = (DB + 2 + 3) / 4 * 4;
+    static constexpr u32 FLAG_D1 = 1u << 30, FLAG_N3 = 1u << 31;  // any flag: w1 >= FLAG_D1
+    static constexpr int F0 = (DB + 3) / 4 * 4;
     // C += 3S + N3 (N3 = 3n + 1, NN limbs).  A C limb sum is < 5B, so its
     // carry (0..4) is a multiply-high by MAGIC = ceil(2^32 / (ES B)) (exact
     // over the range: static_assert).
@@ -119,7 +120,7 @@ struct Cfg {
     static_assert(TB >= (int)EBT && TB - (int)EBT < 65536 && (!LSD || TL < 65536), "LDS offsets");
     static_assert(LDS_BYTES <= 163840, "LDS");
     static_assert(W0 + W <= NBINS, "window");
-    static_assert(!LSD || (ES == 8 && DB > 0 && FC + 6 <= 32), "low-digit entry layout");
+    static_assert(!LSD || (ES == 8 && DB > 0 && FC + 6 <= 30), "low-digit entry layout");
     static_assert(C1 || ((unsigned long long)MAGICB * B - (1ull << 32)) * (TMAX / ES) < (1ull << 32),
                   "C-limb carry magic");
     static_assert(NN <= SL && NE >= NS, "C += 3S + N3 layout");
@@ -133,6 +134,13 @@ __device__ __forceinline__ u32 mad_u24(u32 a, u32 c) {
     static_assert(K <= 64, "inline constant");
     u32 r;
     asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "n"(K), "v"(c));
+    return r;
+}
+
+// v_bcnt_u32_b32 with a scalar accumulator: popcount(x) + acc.
+__device__ __forceinline__ u32 bcnt_acc(u32 x, u32 acc) {
+    u32 r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "s"(acc));
     return r;
 }
 
@@ -294,31 +302,44 @@ __device__ __forceinline__ void carry_n3(State<P> &st) {
     }
 }
 
+// Rare path: a limb-0 wrap of D1 / N3, or a carry out of the top stepped
+// limb of S (tS >= 2^SH, biased) or C (tC >= ES B).  The top stepped limbs
+// are left unreduced by step(): they only take carries, so they need
+// reducing only here.
 template <class P>
-__device__ __forceinline__ void rare(State<P> &st, const unsigned char *smem, u32 d1w, u32 e2w, u32 cS,
-                                     u32 cC, u32 cE) {
-    (void)cE;
+__device__ __forceinline__ void rare(State<P> &st, const unsigned char *smem, u32 d1w, u32 n3w, bool cS,
+                                     bool cC) {
     if (d1w) carry_scaled<P>(st.D1, 1);
-    if (e2w) carry_n3<P>(st);
-    if (cS) carry_plain<P>(st.S, P::SL);
-    if (cC) carry_plain<P>(st.C, P::CL);
+    if (n3w) carry_n3<P>(st);
+    if (cS) {
+        st.S[P::SL - 1] -= P::ESB;
+        carry_plain<P>(st.S, P::SL);
+    }
+    if (cC) {
+        st.C[P::CL - 1] -= P::DC;
+        carry_plain<P>(st.C, P::CL);
+    }
     if (cS | cC) recompute_hi<P>(st, smem);
 }
 
 // One FD step n -> n+1.  w1 = word 1 of the low-digit entry of n (LSD bases):
 // limb 0 of every quantity lives in the table, so the chains start at limb 1
 // with the table's carries.  The carry leaves each limb as c8 = ES * carry,
-// (t >> T) & ES; the limb is reduced with one v_mad_i32_i24.
+// (t >> T) & ES; the limb is reduced with one v_mad_i32_i24.  The top stepped
+// limb of S and of C only ever receives a carry (D1 and 3S + N3 are shorter),
+// so it is just compared: a carry out of it (~1/B per step) goes to rare().
 template <class P>
 __device__ __forceinline__ void step(State<P> &st, const unsigned char *smem, u32 w1) {
     constexpr u32 ES = P::ES;
     constexpr int L0 = P::LO;  // LSD bases: limb 0 lives in the low-digit table
+    constexpr int CT = P::CL - 1, ST = P::SL - 1;  // top stepped limbs
+    static_assert(CT >= P::NS && CT >= P::NN && ST >= P::ND, "top limbs take carries only");
     // C += 3S + N3 (old S), limbs L0 .. CL-1.  Unbiased scaled limbs; a limb
     // sum is < 5B, its carry (0..4) is a multiply-high.
     u32 cC = 0;
     if constexpr (P::LSD) cC = __builtin_amdgcn_ubfe(w1, P::FC, 6);
 #pragma unroll
-    for (int i = L0; i < P::CL; i++) {
+    for (int i = L0; i < CT; i++) {
         u32 t = st.C[i] + cC;
         if (i < P::NN) t += st.N3[i];
         else if (i < P::SL) t -= 3 * P::EBT;
@@ -329,28 +350,31 @@ __device__ __forceinline__ void step(State<P> &st, const unsigned char *smem, u3
         st.C[i] = t - c * P::DC;
         cC = c * ES;
     }
+    st.C[CT] += cC;  // < DC + 4 ES: a carry out is at most 1
     // S += D1, limbs L0 .. SL-1 (biased: carry = bit T of t >> log2 ES).
     u32 cS = 0;
     if constexpr (P::LSD) cS = __builtin_amdgcn_ubfe(w1, P::F0, 4);
 #pragma unroll
-    for (int i = L0; i < P::SL; i++) {
+    for (int i = L0; i < ST; i++) {
         u32 t = st.S[i] + (i < P::ND ? st.D1[i] : 0u) + cS;
         cS = (t >> P::T) & ES;
         st.S[i] = t - cS * P::B;
     }
+    st.S[ST] += cS;
     st.r8 += ES;
+    const bool topS = st.S[ST] >= (1u << P::SH), topC = st.C[CT] >= P::DC;
     if constexpr (P::LSD) {
-        if (((w1 & P::FLAGS) | cS | cC) != 0)
-            rare<P>(st, smem, w1 & (1u << P::DB), w1 & (2u << P::DB), cS, cC, 0);
+        if (w1 >= P::FLAG_D1 || topS || topC)
+            rare<P>(st, smem, w1 & P::FLAG_D1, w1 & P::FLAG_N3, topS, topC);
     } else {
         // limb 0 of D1 (+2) and N3 (+3, stored offset by -3 ES BT) step here
         st.D1[0] += 2 * ES;
         st.N3[0] += 3 * ES;
         const u32 d1w = st.D1[0] >= P::ESB, n3w = st.N3[0] + 3 * P::EBT >= P::ESB;
-        if ((cS | cC | d1w | n3w) != 0) {
+        if (d1w || n3w || topS || topC) {
             if (d1w) st.D1[0] -= P::ESB;
             if (n3w) st.N3[0] -= P::ESB;
-            rare<P>(st, smem, d1w, n3w, cS, cC, 0);
+            rare<P>(st, smem, d1w, n3w, topS, topC);
         }
     }
 }
@@ -388,8 +412,8 @@ __device__ __forceinline__ void fd2_body(u64 start_lo, u64 start_hi, u32 nunits,
             mark(s0);
             mark(c0);
             const u32 d1 = (2 * e + 1) % B, n3 = (3 * e + 1) % B;
-            v[1] |= (d1 + 2 >= B ? 1u : 0u) << P::DB;                // D1 limb-0 wrap
-            v[1] |= (n3 + 3 >= B ? 2u : 0u) << P::DB;                // N3 limb-0 wrap
+            v[1] |= d1 + 2 >= B ? P::FLAG_D1 : 0u;                   // D1 limb-0 wrap
+            v[1] |= n3 + 3 >= B ? P::FLAG_N3 : 0u;                   // N3 limb-0 wrap
             v[1] |= (s0 + d1 >= B ? 8u : 0u) << P::F0;               // S  += D1 carry
             v[1] |= (P::ES * ((c0 + 3 * s0 + n3) / B)) << P::FC;      // C += 3S + N3 carry
             put(smem + P::TL + e * P::ES);
@@ -434,9 +458,11 @@ __device__ __forceinline__ void fd2_body(u64 start_lo, u64 start_hi, u32 nunits,
                 for (int q = P::LO; q < P::CL; q++)
                     or_entry<P>(smem + P::TB + st.C[q], m);
             }
-            u32 uw = (u32)(-P::W0);
+            // uw = unique count - W0: the bias rides in the first v_bcnt's
+            // accumulator operand (an SGPR; LLVM would add it separately).
+            u32 uw = bcnt_acc(m[0], (u32)(-P::W0));
 #pragma unroll
-            for (int w = 0; w < P::MW; w++) uw += __popc(m[w]);
+            for (int w = 1; w < P::MW; w++) uw += __popc(m[w]);
             if (uw < (u32)P::W) {
                 if constexpr (P::PROBE & 2) probe_acc++;
                 else atomicAdd((u32 *)(smem + uw * (P::HROW * 4) + hbase), hinc);
@@ -508,7 +534,6 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
     u64 left = p.count;
     while (left) {
         const u64 cnt = left < max_count ? left : max_count;
-        // Chunks of <= B numbers (low-digit table), about 3 per lane.
         // Chunks of <= B numbers (low-digit table), about 3 per lane, and never
         // more units than lanes x units-per-lane: a lane with one unit more
         // than the rest runs alone at the end (989 such units on the b40 1e9
