@@ -3,10 +3,12 @@
 (BASELINE.json metric; benchmark.rs:60 ExtraLarge field).
 
 One step = one pass of the hot path over one field in BOTH modes: a detailed
-pass (histogram + near-misses) and a niceonly pass (host MSD filter + GPU
-stride candidates), exactly what the reference client does per field
-(client/src/main.rs:120-208, process_range_*_gpu).  Inputs are the field
-bounds only (no host buffers): the kernels derive every n themselves.
+pass (histogram + near-misses) and a niceonly pass (MSD filter + stride
+candidates), what the reference client does per field in either mode
+(client/src/main.rs:120-208, process_range_*_gpu).  The two passes run at once
+on two HIP streams of the GPU (nice_amd.BothModes; --sequential runs them one
+after the other).  Inputs are the field bounds only (no host buffers): the
+kernels derive every n themselves.
 
 Multi-GPU (one process per GPU, torchrun): weak scaling -- N GPUs process one
 N x 1e9 field of base 40, [start, start + N*1e9); rank r takes the r-th
@@ -25,6 +27,14 @@ import json
 import os
 import sys
 import time
+
+# Hardware queues per process (HIP's default is 4): torch's stream, RCCL's
+# stream and the two mode streams of BothModes must not share a queue, or the
+# niceonly pass serialises behind the detailed kernel (torchrun 1 rank: 2.86
+# ms per step with 4 queues, 2.61 with 8).  Set before HIP initialises; an
+# exported value below 8 (the box exports HIP's default, 4) is raised.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -47,6 +57,9 @@ def parse():
     p.add_argument("--msd-floor", type=int, default=0, help="0 = reference CPU-path floor 250")
     p.add_argument("--msd-where", choices=["auto", "host", "device"], default="auto",
                    help="niceonly MSD filter placement (same candidate set either way)")
+    p.add_argument("--sequential", action="store_true",
+                   help="run the two modes one after the other on one stream (default: at once, "
+                        "on two streams of the GPU, nice_amd.BothModes)")
     return p.parse_args()
 
 
@@ -130,6 +143,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # The JSON line is the only thing on stdout: runtime banners (RCCL prints
+    # its version block to fd 1 when the communicator comes up) go to stderr.
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     # Any torchrun launch (WORLD_SIZE set, even 1) takes the distributed path:
     # one RCCL communicator, histogram all-reduce + list all-gather per step.
     if "WORLD_SIZE" in os.environ:
@@ -141,6 +158,9 @@ def main():
     import nice_amd as N
 
     ctx = N.GpuContext([local])
+    # Both modes of a field at once: niceonly's launch-bound MSD levels run on
+    # a second stream beside the detailed kernel (nice_amd.BothModes).
+    runner = N.BothModes(local, det_ctx=ctx) if args.mode == "both" and not args.sequential else ctx
     br = N.get_base_range_u128(BASE)
     start, end = rank_field(br.range_start, rank)
     assert end <= br.range_end
@@ -154,7 +174,7 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    det_ms, nice_ms, kern_ms = [], [], []
+    det_ms, nice_ms, kern_ms, both_ms = [], [], [], []
     last_nice_stats = None
     from nice_amd import dist as D
     whole = N.FieldSize(br.range_start, br.range_start + world * FIELD_SIZE)
@@ -175,11 +195,21 @@ def main():
             # with the next step's compute (nice_amd/dist.py PipelinedExchange);
             # the previous step's results come back here and are checked.
             t = time.perf_counter()
-            done = D.process_field_both_pipelined(ex, whole, BASE, ctx, msd_floor=args.msd_floor,
+            done = D.process_field_both_pipelined(ex, whole, BASE, runner, msd_floor=args.msd_floor,
                                                   msd_where=args.msd_where)
             det_ms.append((time.perf_counter() - t) * 1e3)
             kern_ms.append(ctx.kernel_stats().kernel_ms)
             check_both(done)
+            return
+        if runner is not ctx and dist is None:
+            # single GPU, both modes at once: one wall time for the pair
+            t = time.perf_counter()
+            (hist, _), (_, st) = runner.both_raw((start, end), (start, end), BASE,
+                                                 msd_floor=args.msd_floor, msd_where=args.msd_where)
+            both_ms.append((time.perf_counter() - t) * 1e3)
+            kern_ms.append(ctx.kernel_stats().kernel_ms)
+            assert sum(hist) == FIELD_SIZE
+            last_nice_stats = st
             return
         if args.mode in ("both", "detailed"):
             t = time.perf_counter()
@@ -215,7 +245,7 @@ def main():
     for _ in range(args.warmup):
         step()
     drain()
-    det_ms.clear(), nice_ms.clear(), kern_ms.clear()
+    det_ms.clear(), nice_ms.clear(), kern_ms.clear(), both_ms.clear()
 
     elapsed = timed(step, args.steps, barrier_sync, dist, tail=drain)
 
@@ -223,6 +253,8 @@ def main():
     total_numbers = modes * FIELD_SIZE * world * args.steps
     value = total_numbers / elapsed
     if rank != 0:
+        if runner is not ctx:
+            runner.close()
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -270,6 +302,9 @@ def main():
                     "HBM bytes per launch from the committed PMC pass (profiles/r01/traffic.json, "
                     "FETCH_SIZE x2 + WRITE_SIZE), the field's bounds are the only input",
         }
+    line["modes_overlapped"] = runner is not ctx
+    if both_ms:
+        line["both_wall_ms"] = sum(both_ms) / len(both_ms)  # detailed + niceonly at once
     if det_ms:
         line["detailed_numbers_per_sec"] = FIELD_SIZE / (sum(det_ms) / len(det_ms) / 1e3)
         line["detailed_ms"] = sum(det_ms) / len(det_ms)
@@ -277,13 +312,15 @@ def main():
         line["niceonly_numbers_per_sec"] = FIELD_SIZE / (sum(nice_ms) / len(nice_ms) / 1e3)
         line["niceonly_ms"] = sum(nice_ms) / len(nice_ms)
     st = last_nice_stats
-    if st is not None and (nice_ms or dist is not None):
+    if st is not None and (nice_ms or both_ms or dist is not None):
         line["niceonly"] = {"ranges": st.ranges, "range_numbers": st.range_numbers,
                             "candidates": st.candidates, "launches": st.launches,
                             "msd_seconds": st.msd_seconds, "total_seconds": st.total_seconds}
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(br.range_start, args.cpu_seconds)
-    print(json.dumps(line), flush=True)
+    print(json.dumps(line), file=json_out, flush=True)
+    if runner is not ctx:
+        runner.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -204,6 +204,15 @@ class GpuContext:
                                   st.msd_seconds, st.total_seconds)
             return lst, stats
 
+    # -- both modes of one field ---------------------------------------------
+    def both_raw(self, det_range, nice_range, base: int, **nice_opts):
+        """Detailed of det_range and niceonly of nice_range (either None to
+        skip), one after the other on this context's stream.  Returns
+        ((hist, near_misses), (nice, stats)); BothModes runs the two at once."""
+        det = self.detailed_raw(*det_range, base) if det_range else (None, [])
+        nice = self.niceonly_raw(*nice_range, base, **nice_opts) if nice_range else ([], None)
+        return det, nice
+
     def debug_unique_counts(self, ns: Sequence[int], base: int) -> List[int]:
         arr = (ctypes.c_uint64 * (2 * max(len(ns), 1)))()
         for i, n in enumerate(ns):
@@ -219,6 +228,79 @@ class GpuContext:
         out = (ctypes.c_uint32 * max(len(ns), 1))()
         check(lib().nice_debug_is_nice(self._h, arr, len(ns), base, out))
         return [bool(x) for x in out[: len(ns)]]
+
+
+class BothModes:
+    """Detailed and niceonly of one field at the same time on one GPU.
+
+    Each mode gets its own context, i.e. its own HIP stream, and the niceonly
+    pass is driven from a worker thread (ctypes releases the GIL for the
+    call), so its launch-latency-bound MSD levels and candidate kernel run
+    beside the detailed kernel instead of after it: the b40 1e9 bench step
+    goes from 2.63 to 2.48 ms (scripts/overlap_probe.py).  Same results as
+    GpuContext.both_raw, which runs the two in sequence."""
+
+    def __init__(self, device: int = 0, det_ctx: Optional[GpuContext] = None,
+                 nice_ctx: Optional[GpuContext] = None):
+        self.det = det_ctx if det_ctx is not None else GpuContext([device])
+        self.nice = nice_ctx if nice_ctx is not None else GpuContext([device])
+        self._own_nice = nice_ctx is None
+        self._go = threading.Event()
+        self._done = threading.Event()
+        self._job = None
+        self._res = None
+        self._closed = False
+        self._thread = threading.Thread(target=self._serve, name="nice-niceonly", daemon=True)
+        self._thread.start()
+
+    def _serve(self):
+        while True:
+            self._go.wait()
+            self._go.clear()
+            if self._closed:
+                return
+            args, kw = self._job
+            try:
+                self._res = (True, self.nice.niceonly_raw(*args, **kw))
+            except BaseException as e:  # re-raised on the calling thread
+                self._res = (False, e)
+            self._done.set()
+
+    def kernel_stats(self, device_index: int = 0) -> KernelStats:
+        """The detailed pass's kernel statistics."""
+        return self.det.kernel_stats(device_index)
+
+    def detailed_raw(self, *a, **kw):
+        return self.det.detailed_raw(*a, **kw)
+
+    def niceonly_raw(self, *a, **kw):
+        return self.nice.niceonly_raw(*a, **kw)
+
+    def both_raw(self, det_range, nice_range, base: int, **nice_opts):
+        if self._closed:
+            raise RuntimeError("BothModes is closed")
+        if not nice_range:
+            return (self.det.detailed_raw(*det_range, base) if det_range else (None, [])), ([], None)
+        self._job = ((*nice_range, base), nice_opts)
+        self._done.clear()
+        self._go.set()
+        try:
+            det = self.det.detailed_raw(*det_range, base) if det_range else (None, [])
+        finally:
+            self._done.wait()
+        ok, nice = self._res
+        self._res = None
+        if not ok:
+            raise nice
+        return det, nice
+
+    def close(self):
+        if not self._closed:
+            self._closed = True
+            self._go.set()
+            self._thread.join()
+            if self._own_nice:
+                self.nice.close()
 
 
 def process_range_detailed_gpu(ctx: GpuContext, range_: FieldSize, base: int) -> FieldResults:

@@ -51,7 +51,14 @@ namespace fd2 {
 constexpr int log2ceil(unsigned v) { int t = 0; while ((1u << t) < v) t++; return t; }
 constexpr int ilog2(unsigned v) { int t = 0; while ((2u << t) <= v) t++; return t; }
 
-template <int BASE_, int ND_, int NE_, int NE2_, int PROBE_ = 0, int WG_ = 512>
+// Exactness of the digit split q = mulhi(ES v, m) = v / b over v < b^2.
+constexpr bool split_exact(unsigned base, unsigned es, unsigned long long m) {
+    for (unsigned v = 0; v < base * base; v++)
+        if (((unsigned long long)es * v * m) >> 32 != v / base) return false;
+    return true;
+}
+
+template <int BASE_, int ND_, int NE_, int NE2_, int PROBE_ = 0, int WG_ = 512, int VD_ = 0>
 struct Cfg {
     static constexpr int BASE = BASE_;
     // Bottleneck probes (timing experiments only, results are wrong): 1 = no
@@ -111,6 +118,13 @@ struct Cfg {
     static constexpr bool C1 = ((unsigned long long)MAGIC * DC - (1ull << 32)) * TMAX < (1ull << 32);
     static constexpr u32 MAGICB = (u32)(((1ull << 32) + B - 1) / B);
     static constexpr int FC = F0 + 4;  // 6-bit field: ES * (carry out of C limb 0)
+    // VALU-decoded limbs (no table lookup): 1 = top stepped C limb, 2 = also
+    // the top stepped S limb.  Their two digits come from one multiply-high
+    // by MAGIC_D = ceil(2^32 / (ES b)) and set their bits with 64-bit shifts,
+    // trading ~6 VALU ops for one data-random (bank-conflicting) LDS read.
+    static constexpr int VD = VD_;
+    static constexpr u32 MAGIC_D = (u32)(((1ull << 32) + ES * BASE - 1) / (ES * BASE));
+    static_assert(VD == 0 || (MW == 2 && ES == 8 && split_exact(BASE, ES, MAGIC_D)), "VALU digit split");
     // Waves per SIMD the LDS allows (the VGPR budget is set to match).
     static constexpr int WPE0 = (163840 / LDS_BYTES) * (WG / 64) / 4;
     static constexpr int WPE = WPE0 > 8 ? 8 : WPE0;
@@ -168,6 +182,16 @@ __device__ __forceinline__ void or_entry(const unsigned char *p, u32 (&m)[P::MW]
         m[1] |= v.y;
         m[2] |= v.z;
     }
+}
+
+// Digit bits of a scaled limb (ES = 8, v8 = 8 v, v < B) by VALU.
+template <class P>
+__device__ __forceinline__ void or_valu(u32 v8, u32 (&m)[P::MW]) {
+    const u32 q = __umulhi(v8, P::MAGIC_D);       // high digit
+    const u32 r = (v8 >> 3) - q * (u32)P::BASE;   // low digit
+    const u64 bits = (1ull << q) | (1ull << r);
+    m[0] |= (u32)bits;
+    m[1] |= (u32)(bits >> 32);
 }
 
 template <class P>
@@ -453,10 +477,15 @@ __device__ __forceinline__ void fd2_body(u64 start_lo, u64 start_hi, u32 nunits,
                     w1 = v.y;
                 }
 #pragma unroll
-                for (int q = P::LO; q < P::SL; q++) or_entry<P>(smem + (P::TB - P::EBT) + st.S[q], m);
+                for (int q = P::LO; q < P::SL; q++) {
+                    if (P::VD >= 2 && q == P::SL - 1) or_valu<P>(st.S[q] - P::EBT, m);
+                    else or_entry<P>(smem + (P::TB - P::EBT) + st.S[q], m);
+                }
 #pragma unroll
-                for (int q = P::LO; q < P::CL; q++)
-                    or_entry<P>(smem + P::TB + st.C[q], m);
+                for (int q = P::LO; q < P::CL; q++) {
+                    if (P::VD >= 1 && q == P::CL - 1) or_valu<P>(st.C[q], m);
+                    else or_entry<P>(smem + P::TB + st.C[q], m);
+                }
             }
             // uw = unique count - W0: the bias rides in the first v_bcnt's
             // accumulator operand (an SGPR; LLVM would add it separately).
@@ -680,6 +709,8 @@ static hipError_t launch_segment(const DetailedLaunch &p, int num_cus, hipStream
         // (6 waves/SIMD) tie at 2.56-2.58 ms, 1024 (8 waves, spills) 2.59,
         // 896 (7 waves) 2.85-2.92, 640 (5 waves) 3.18.
         if (probe == 6) return launch_cfg<Cfg<40, 4, 8, 5, 0, 768>>(p, num_cus, s);
+        if (probe == 8) return launch_cfg<Cfg<40, 4, 8, 5, 0, 512, 1>>(p, num_cus, s);
+        if (probe == 9) return launch_cfg<Cfg<40, 4, 8, 5, 0, 512, 2>>(p, num_cus, s);
     }
 #define X(B_, ND_, NE_, NE2_)                                              \
     if (p.base == B_ && c.nd == ND_ && c.ne == NE_ && c.ne2 == NE2_)        \

@@ -131,6 +131,21 @@ def niceonly_shard_bounds(range_: FieldSize, rank: int, world: int, chunk: int =
     return s, e, chunk
 
 
+def _both_shards(range_: FieldSize, base: int, ctx, rank: int, world: int, nice_opts):
+    """This rank's detailed shard and niceonly shard of `range_`, through
+    ctx.both_raw when the context has it (GpuContext: in sequence; BothModes:
+    at once, on two streams), else detailed_raw then niceonly_raw."""
+    s, e = shard_bounds(range_.range_start, range_.range_end, rank, world)
+    ns, ne, chunk = niceonly_shard_bounds(range_, rank, world, nice_opts.pop("chunk_size", 0))
+    nice_range = (ns, ne) if ns < ne else None
+    if hasattr(ctx, "both_raw"):
+        return ctx.both_raw((s, e), nice_range, base, chunk_size=chunk, **nice_opts)
+    det = ctx.detailed_raw(s, e, base)
+    nice = ctx.niceonly_raw(ns, ne, base, chunk_size=chunk, **nice_opts) if nice_range \
+        else ([], None)
+    return det, nice
+
+
 def process_field_both_dist(range_: FieldSize, base: int, ctx, group=None,
                             **nice_opts):
     """Detailed AND niceonly of one field over a process group with ONE
@@ -140,11 +155,7 @@ def process_field_both_dist(range_: FieldSize, base: int, ctx, group=None,
     niceonly statistics or None)."""
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    s, e = shard_bounds(range_.range_start, range_.range_end, rank, world)
-    hist, near = ctx.detailed_raw(s, e, base)
-    ns, ne, chunk = niceonly_shard_bounds(range_, rank, world, nice_opts.pop("chunk_size", 0))
-    nice, stats = ctx.niceonly_raw(ns, ne, base, chunk_size=chunk, **nice_opts) if ns < ne \
-        else ([], None)
+    (hist, near), (nice, stats) = _both_shards(range_, base, ctx, rank, world, nice_opts)
     red = _all_reduce_ints(list(hist[: base + 1]) + _onehot(rank, world, len(near))
                            + _onehot(rank, world, len(nice)), dist, group)
     hist = red[: base + 1]
@@ -224,11 +235,7 @@ def process_field_both_pipelined(ex: PipelinedExchange, range_: FieldSize, base:
     the last field's."""
     dist, group = ex.dist, ex.group
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    s, e = shard_bounds(range_.range_start, range_.range_end, rank, world)
-    hist, near = ctx.detailed_raw(s, e, base)
-    ns, ne, chunk = niceonly_shard_bounds(range_, rank, world, nice_opts.pop("chunk_size", 0))
-    nice, stats = ctx.niceonly_raw(ns, ne, base, chunk_size=chunk, **nice_opts) if ns < ne \
-        else ([], None)
+    (hist, near), (nice, stats) = _both_shards(range_, base, ctx, rank, world, nice_opts)
     vec = list(hist[: base + 1]) + _onehot(rank, world, len(near)) + _onehot(rank, world, len(nice))
     return finish_both(ex, ex.submit(vec, (base, near, nice, stats)))
 

@@ -111,6 +111,15 @@ def _field_worker(rank, world, port, q):
     res["pipelined"] = [([(d.num_uniques, d.count) for d in r[0].distribution],
                          [(n.number, n.num_uniques) for n in r[0].nice_numbers],
                          [n.number for n in r[1].nice_numbers]) for r in got[1:]]
+    # the same through BothModes (the two modes at once, bench.py's default)
+    from nice_amd import BothModes
+    both = BothModes(det_ctx=_OracleCtx(), nice_ctx=_OracleCtx())
+    got = [D.process_field_both_pipelined(ex, f, 10, both, chunk_size=997) for f in fields]
+    got.append(D.finish_both(ex, ex.drain()))
+    both.close()
+    res["pipelined_both"] = [([(d.num_uniques, d.count) for d in r[0].distribution],
+                              [(n.number, n.num_uniques) for n in r[0].nice_numbers],
+                              [n.number for n in r[1].nice_numbers]) for r in got[1:]]
     q.put((rank, res))
     dist.destroy_process_group()
 
@@ -145,7 +154,34 @@ def test_two_rank_field_sharding_matches_single_process():
         w = O.process_range_detailed(a, a + 2_000, 10)
         assert r == (w.distribution, w.nice_numbers, _oracle_niceonly_shard(a, a + 2_000, 10, 997))
     assert out[0]["pipelined"][0][2] == [69]
+    assert out[0]["pipelined_both"] == out[0]["pipelined"]
     # shard cuts fall on the whole field's chunk grid
     assert D.shard_bounds(0, 10 ** 6, 0, 2, 99_991)[1] % 99_991 == 0
     assert D.shard_bounds(0, 10, 1, 3) == (4, 7)
     assert D.client_chunk_size(10 ** 9) == 10 ** 6 and D.client_chunk_size(10 ** 13) == 10 ** 8
+
+
+def test_both_modes_runner_matches_sequential_and_propagates_errors():
+    """BothModes (nice_amd/api.py): niceonly on a worker thread beside the
+    detailed call; same results as the two calls in sequence, and an error
+    raised by the niceonly pass surfaces on the calling thread."""
+    from nice_amd import BothModes
+    both = BothModes(det_ctx=_OracleCtx(), nice_ctx=_OracleCtx())
+    try:
+        for a in (47, 10 ** 6 - 53):
+            (h, near), (nice, _) = both.both_raw((a, a + 1_500), (a, a + 1_500), 10, chunk_size=500)
+            ref = _OracleCtx()
+            assert (h, near) == ref.detailed_raw(a, a + 1_500, 10)
+            assert nice == ref.niceonly_raw(a, a + 1_500, 10, chunk_size=500)[0]
+        (h, _), (nice, st) = both.both_raw((47, 100), None, 10)
+        assert nice == [] and st is None and sum(h) == 53
+
+        class Boom(_OracleCtx):
+            def niceonly_raw(self, *a, **k):
+                raise ValueError("boom")
+        bad = BothModes(det_ctx=_OracleCtx(), nice_ctx=Boom())
+        with pytest.raises(ValueError, match="boom"):
+            bad.both_raw((47, 100), (47, 100), 10)
+        bad.close()
+    finally:
+        both.close()

@@ -340,3 +340,29 @@ def test_multi_device_context_sharding():
     hist, lst = c.detailed_raw(s, s + 100_001, 40)
     assert _dist(hist) == want.distribution and lst == want.nice_numbers
     c.close()
+
+
+def test_both_modes_overlapped_matches_fixtures(ctx):
+    # BothModes (bench.py's default): niceonly on a second stream beside the
+    # detailed kernel; both results must equal the committed full-field
+    # fixtures, repeatedly (the two streams share the device).
+    fields = _oracle_fields()
+    det = {c["name"]: c for c in fields["detailed"]}
+    b = N.BothModes(0, det_ctx=ctx)
+    try:
+        for c in fields["niceonly"]:
+            s, e, base = int(c["start"]), int(c["end"]), c["base"]
+            d = next((x for x in det.values() if (int(x["start"]), int(x["end"]), x["base"])
+                      == (s, e, base)), None)
+            for _ in range(2):
+                (hist, near), (nice, st) = b.both_raw((s, e), (s, e), base)
+                assert st.candidates == c["candidates"], c["name"]
+                assert [str(n) for n in nice] == c["nice_numbers"], c["name"]
+                assert sum(hist) == e - s
+                if d is not None:
+                    assert _dist(hist) == [tuple(x) for x in d["distribution"]], c["name"]
+                    assert near == [(int(n), u) for n, u in d["near_misses"]], c["name"]
+        (hist, near), (nice, _) = b.both_raw((47, 100), (47, 100), 10)
+        assert near == [(69, 10)] and nice == [69]
+    finally:
+        b.close()
