@@ -286,6 +286,7 @@ def main():
     }
     if dist is not None and args.mode == "both":
         line["rank_step_ms"] = sum(det_ms) / len(det_ms)  # both modes + exchange, rank 0
+        line["rank_step_ms_median"] = sorted(det_ms)[len(det_ms) // 2]
         det_ms.clear()  # not split per mode on this path
         line["detailed_kernel_ms"] = sum(kern_ms) / len(kern_ms)
     if kern_ms:
@@ -305,6 +306,7 @@ def main():
     line["modes_overlapped"] = runner is not ctx
     if both_ms:
         line["both_wall_ms"] = sum(both_ms) / len(both_ms)  # detailed + niceonly at once
+        line["both_wall_ms_median"] = sorted(both_ms)[len(both_ms) // 2]
     if det_ms:
         line["detailed_numbers_per_sec"] = FIELD_SIZE / (sum(det_ms) / len(det_ms) / 1e3)
         line["detailed_ms"] = sum(det_ms) / len(det_ms)

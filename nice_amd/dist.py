@@ -176,8 +176,11 @@ class PipelinedExchange:
     returns the PREVIOUS field's reduced vector; drain() returns the last one.
     The lists of a field are gathered when its vector is collected (only if
     non-empty, which is rare).  Two preallocated device vectors alternate, fed
-    from / read back into pinned host memory, so a step costs one async copy
-    each way and one collective launch."""
+    from / read back into pinned host memory; on a GPU the read-back is queued
+    behind the collective at submit time and marked by an event, so a step
+    costs three asynchronous enqueues and collecting the previous field only
+    waits on an event that has long fired (no synchronous copy on the
+    launching thread)."""
 
     def __init__(self, dist, group=None, width: int = 0):
         self.dist, self.group = dist, group
@@ -195,6 +198,7 @@ class PipelinedExchange:
         self.bufs = [(torch.zeros(width, dtype=torch.int64, pin_memory=pin),
                       torch.zeros(width, dtype=torch.int64, device=dev),
                       torch.zeros(width, dtype=torch.int64, pin_memory=pin)) for _ in range(2)]
+        self.events = [torch.cuda.Event() for _ in range(2)] if pin else None
         self.width = width
 
     def submit(self, vals: Sequence[int], payload):
@@ -202,10 +206,18 @@ class PipelinedExchange:
             self.drain_check()
             self._alloc(len(vals))
         h_in, d, h_out = self.bufs[self.flip]
+        ev = self.events[self.flip] if self.events is not None else None
         self.flip ^= 1
         h_in.numpy()[:] = vals
         d.copy_(h_in, non_blocking=True)
         work = self.dist.all_reduce(d, op=self.dist.ReduceOp.SUM, group=self.group, async_op=True)
+        if ev is not None:
+            # device: the current stream waits for the collective (no host
+            # block), then the read-back is queued and marked
+            work.wait()
+            h_out.copy_(d, non_blocking=True)
+            ev.record()
+            work = ev
         prev, self.pending = self.pending, (work, d, h_out, payload)
         return self._collect(prev)
 
@@ -221,8 +233,11 @@ class PipelinedExchange:
         if p is None:
             return None
         work, d, h_out, payload = p
-        work.wait()
-        h_out.copy_(d)  # synchronises with the collective's stream
+        if self.events is not None:
+            work.synchronize()  # the read-back queued at submit time
+        else:
+            work.wait()
+            h_out.copy_(d)
         return h_out.tolist(), payload
 
 

@@ -6,7 +6,8 @@ import statistics
 import sys
 import time
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
@@ -19,6 +20,9 @@ if use_dist:
     dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 else:
     local = 0
+    if os.environ.get("TORCH_CUDA"):
+        import torch
+        torch.zeros(1, device="cuda")
 import nice_amd as N  # noqa: E402
 from nice_amd import dist as D  # noqa: E402
 
@@ -39,8 +43,10 @@ def med(fn, reps=20):
     return round(statistics.median(ts) * 1e3, 4)
 
 
-tag = "dist" if use_dist else "plain"
+tag = "dist" if use_dist else ("plain+torch" if os.environ.get("TORCH_CUDA") else "plain")
 print(tag, "both_raw", med(lambda: both.both_raw((s, e), (s, e), 40)), flush=True)
+print(tag, "detailed", med(lambda: ctx.detailed_raw(s, e, 40)), flush=True)
+print(tag, "niceonly", med(lambda: ctx.niceonly_raw(s, e, 40)), flush=True)
 print(tag, "sequential", med(lambda: ctx.both_raw((s, e), (s, e), 40)), flush=True)
 if use_dist:
     ex = D.PipelinedExchange(dist)
