@@ -181,6 +181,10 @@ __device__ __forceinline__ void or_entry(const unsigned char *p, u32 (&m)[P::MW]
         m[0] |= v.x;
         m[1] |= v.y;
         m[2] |= v.z;
+        // Keep the 4th (zero) dword live so the load stays ds_read_b128: LLVM
+        // would shrink it to ds_read_b96, which gfx950 serves in 8 lane groups
+        // over 32 banks (8 cycles per wave) instead of 4 groups over 64 (4).
+        asm volatile("" ::"v"(v.w));
     }
 }
 
