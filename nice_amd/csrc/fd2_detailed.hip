@@ -572,7 +572,8 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         // than the rest runs alone at the end (989 such units on the b40 1e9
         // field once cost ~7 % of the launch).
         const u64 per_lane = (cnt + lanes - 1) / lanes;
-        u64 upl = (per_lane + P::B - 1) / P::B < 3 ? 3 : (per_lane + P::B - 1) / P::B;
+        const u64 upl_min = getenv("NICE_FD2_UPL") ? strtoull(getenv("NICE_FD2_UPL"), 0, 10) : 3;
+        u64 upl = (per_lane + P::B - 1) / P::B < upl_min ? upl_min : (per_lane + P::B - 1) / P::B;
         u64 chunk;
         for (;; upl++) {
             chunk = (cnt + lanes * upl - 1) / (lanes * upl);  // ceil: cnt / chunk <= lanes * upl
@@ -582,9 +583,13 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
             if (chunk < 1) chunk = 1;
             // Odd chunks: lane l of a wave then sits at n mod B = r0 + chunk * l,
             // so its low-digit entries fall on 32 distinct bank pairs per
-            // half-wave (B is a multiple of 32 for the LSD bases): rounding UP
+            // half-wave (B is a multiple of 32 for the LSD bases).  Without a
+            // low-digit table (b80) limb 0 of n^2 and n^3 is looked up in the
+            // pair table, and a chunk divisible by 16 puts a 16-lane group on
+            // ONE bank quad for those lookups (n^2 mod 16 equal on every lane):
+            // b80 1e9 at chunk 2544 took 11.8 ms, at 2545 9.3.  Rounding UP
             // keeps the unit count within lanes x upl.
-            if (P::LSD && chunk > 1 && chunk % 2 == 0) chunk++;
+            if (chunk > 1 && chunk % 2 == 0) chunk++;
             if (chunk <= P::B) break;
         }
         u64 nunits = cnt / chunk;
