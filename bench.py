@@ -108,6 +108,17 @@ def cpu_threads():
     return max(1, min(16, os.cpu_count() or 1))
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(start, target_s):
     """Reference algorithm (oracle/ C restatement, 'port') on the host cores,
     on a bounded sample of the same workload, extrapolated per number."""
@@ -130,7 +141,20 @@ def cpu_baseline(start, target_s):
     tn = time.perf_counter() - t
     nice_rate = FIELD_SIZE / tn
     combined = 2 * FIELD_SIZE / (FIELD_SIZE / det_rate + tn)
+    # the reference client's default thread count (--threads 4,
+    # client/src/main.rs:94), on a smaller detailed sample
+    n4 = max(1_000_000, int(det_rate / th * 4 * target_s / 3) // 1_000_000 * 1_000_000)
+    t = time.perf_counter()
+    O.process_field_detailed_mt(start, start + n4, BASE, 4)
+    det4 = n4 / (time.perf_counter() - t)
+    t = time.perf_counter()
+    O.process_field_niceonly_mt(start, start + FIELD_SIZE, BASE, 4)
+    tn4 = time.perf_counter() - t
     return {"value": combined, "unit": "numbers/s", "cores": th, "kind": "port",
+            "cpu_model": cpu_model(),
+            "threads4": {"value": 2 * FIELD_SIZE / (FIELD_SIZE / det4 + tn4), "cores": 4,
+                         "detailed_numbers_per_sec": det4, "niceonly_numbers_per_sec": FIELD_SIZE / tn4,
+                         "sample": f"detailed: first {n4:.3g} n; niceonly: whole 1e9 field"},
             "sample": f"detailed: first {n:.3g} n of the field on {th} threads "
                       f"({det_rate:.3e} n/s, extrapolated to 1e9); niceonly: whole 1e9 field "
                       f"({nice_rate:.3e} n/s); reference client chunking, MSD floor 250, k=2",
