@@ -553,10 +553,16 @@ fd2_tail_kernel(u64 start_lo, u64 start_hi, u32 nunits, u32 cutoff, u64 *__restr
 template <class P>
 static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s) {
     auto kern = fd2_kernel<P>;
-    int per_cu = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)kern, P::WG, 0);
-    if (e != hipSuccess) return e;
-    if (per_cu < 1) per_cu = 1;
+    // Occupancy is a property of the code object: queried once per
+    // instantiation (a runtime call per launch is host latency on small fields).
+    static const int per_cu_q = [&] {
+        int v = 0;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, (const void *)kern, P::WG, 0) == hipSuccess
+                   ? v : -1;
+    }();
+    if (per_cu_q < 0) return hipErrorInvalidDeviceFunction;
+    const int per_cu = per_cu_q < 1 ? 1 : per_cu_q;
+    hipError_t e = hipSuccess;
     const u64 lanes = (u64)num_cus * per_cu * P::WG;
     // u16 counters: at most 65535 numbers per lane per launch.
     const u64 max_count = P::HP ? lanes * 60000ull : ~0ull;
@@ -573,13 +579,16 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         // field once cost ~7 % of the launch).
         const u64 per_lane = (cnt + lanes - 1) / lanes;
         const u64 upl_min = getenv("NICE_FD2_UPL") ? strtoull(getenv("NICE_FD2_UPL"), 0, 10) : 3;
+        // Chunk floor for fields too small to fill the chip: a lane's init
+        // costs about ten steps, but with idle CUs latency wins (b40 1e6:
+        // kernel 25 us at a floor of 32, 14 us at 4; scripts/small_fields.py).
+        const u64 min_chunk = getenv("NICE_FD2_MINCHUNK") ? strtoull(getenv("NICE_FD2_MINCHUNK"), 0, 10) : 4;
         u64 upl = (per_lane + P::B - 1) / P::B < upl_min ? upl_min : (per_lane + P::B - 1) / P::B;
         u64 chunk;
         for (;; upl++) {
             chunk = (cnt + lanes * upl - 1) / (lanes * upl);  // ceil: cnt / chunk <= lanes * upl
-            // A lane's init (radix-B conversion, products) costs about ten
-            // steps: small fields use fewer lanes with >= 32 numbers each.
-            if (chunk < 32) chunk = cnt < 32 ? cnt : 32;
+            // Small fields: at least min_chunk numbers per lane (see above).
+            if (chunk < min_chunk) chunk = cnt < min_chunk ? cnt : min_chunk;
             if (chunk < 1) chunk = 1;
             // Odd chunks: lane l of a wave then sits at n mod B = r0 + chunk * l,
             // so its low-digit entries fall on 32 distinct bank pairs per
