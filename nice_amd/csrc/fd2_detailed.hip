@@ -62,7 +62,8 @@ template <int BASE_, int ND_, int NE_, int NE2_, int PROBE_ = 0, int WG_ = 512, 
 struct Cfg {
     static constexpr int BASE = BASE_;
     // Bottleneck probes (timing experiments only, results are wrong): 1 = no
-    // table lookups (limb words OR-ed directly), 2 = no LDS histogram add.
+    // table lookups (limb words OR-ed directly), 2 = no LDS histogram add,
+    // 4 = no limb-1 lookups of S and C.
     static constexpr int PROBE = PROBE_;
     static constexpr int ND = ND_, NE = NE_, NE2 = NE2_;
     static constexpr int k = BASE / 5, r5 = BASE % 5;
@@ -482,11 +483,13 @@ __device__ __forceinline__ void fd2_body(u64 start_lo, u64 start_hi, u32 nunits,
                 }
 #pragma unroll
                 for (int q = P::LO; q < P::SL; q++) {
+                    if ((P::PROBE & 4) && q == 1) { m[0] |= st.S[q] & 0xffu; continue; }  // probe: no limb-1 lookups
                     if (P::VD >= 2 && q == P::SL - 1) or_valu<P>(st.S[q] - P::EBT, m);
                     else or_entry<P>(smem + (P::TB - P::EBT) + st.S[q], m);
                 }
 #pragma unroll
                 for (int q = P::LO; q < P::CL; q++) {
+                    if ((P::PROBE & 4) && q == 1) { m[1] |= st.C[q] & 0xffu; continue; }
                     if (P::VD >= 1 && q == P::CL - 1) or_valu<P>(st.C[q], m);
                     else or_entry<P>(smem + P::TB + st.C[q], m);
                 }
@@ -723,6 +726,7 @@ static hipError_t launch_segment(const DetailedLaunch &p, int num_cus, hipStream
         if (probe == 1) return launch_cfg<Cfg<40, 4, 8, 5, 1>>(p, num_cus, s);
         if (probe == 2) return launch_cfg<Cfg<40, 4, 8, 5, 2>>(p, num_cus, s);
         if (probe == 3) return launch_cfg<Cfg<40, 4, 8, 5, 3>>(p, num_cus, s);
+        if (probe == 4) return launch_cfg<Cfg<40, 4, 8, 5, 4>>(p, num_cus, s);
         // Workgroup-size sweep (profiles/r01/fd2_wg_sweep.log): 512 and 768
         // (6 waves/SIMD) tie at 2.56-2.58 ms, 1024 (8 waves, spills) 2.59,
         // 896 (7 waves) 2.85-2.92, 640 (5 waves) 3.18.
