@@ -710,9 +710,11 @@ static const BaseThresholds &thresholds(uint32_t base) {
 }
 
 // Workgroup size per base.  b80's 102 KB mask table leaves room for one
-// workgroup per CU; 768 threads (3 waves/SIMD) would need <= 168 VGPRs and
-// spills (3.19 ms per 2e8) where 512 threads at 2 waves/SIMD do not (2.83 ms).
-#define WG_FOR(b) 512
+// workgroup per CU, and the kernel is bound by LDS bank conflicts, so it wants
+// as many waves as fit: 1024 threads (4 waves/SIMD, 128 VGPRs with ~100 bytes
+// of cold spills) run the 1e9 field in 8.49 ms against 8.98 at 768 threads
+// and 9.37 at 512 (scripts/b80_probe.py, profiles/r01/b80_wg_sweep.log).
+#define WG_FOR(b) ((b) == 80 ? 1024 : 512)
 #define FD2_COMBOS(X)                                                                           \
     X(40, 4, 8, 5) X(40, 5, 8, 5) X(40, 5, 9, 5) X(50, 5, 10, 6) X(50, 6, 10, 6) X(50, 6, 11, 6) \
         X(80, 8, 16, 9) X(80, 9, 16, 9) X(80, 9, 17, 9)
@@ -733,6 +735,13 @@ static hipError_t launch_segment(const DetailedLaunch &p, int num_cus, hipStream
         if (probe == 6) return launch_cfg<Cfg<40, 4, 8, 5, 0, 768>>(p, num_cus, s);
         if (probe == 8) return launch_cfg<Cfg<40, 4, 8, 5, 0, 512, 1>>(p, num_cus, s);
         if (probe == 9) return launch_cfg<Cfg<40, 4, 8, 5, 0, 512, 2>>(p, num_cus, s);
+    }
+    // b80 fields too small to fill the chip keep 512-thread workgroups (the
+    // per-workgroup table build dominates there: 1e6 kernel 30 vs 38 us).
+    if (p.base == 80 && (probe == 20 || p.count < 10000000ull)) {
+        if (c.nd == 8 && c.ne == 16) return launch_cfg<Cfg<80, 8, 16, 9, 0, 512>>(p, num_cus, s);
+        if (c.nd == 9 && c.ne == 16) return launch_cfg<Cfg<80, 9, 16, 9, 0, 512>>(p, num_cus, s);
+        if (c.nd == 9 && c.ne == 17) return launch_cfg<Cfg<80, 9, 17, 9, 0, 512>>(p, num_cus, s);
     }
 #define X(B_, ND_, NE_, NE2_)                                              \
     if (p.base == B_ && c.nd == ND_ && c.ne == NE_ && c.ne2 == NE2_)        \
