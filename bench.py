@@ -317,7 +317,7 @@ def main():
         kms = sum(kern_ms) / len(kern_ms)
         achieved = W_ALG * FIELD_SIZE / (kms / 1e3) / 1e12
         line["roofline"] = {
-            "bound": "valu", "kernel": "nice::fd2::fd2_kernel<Cfg<40, 4, 8, 5>>",
+            "bound": "valu", "kernel": "nice::fd2::fd2_kernel<Cfg<40, 4, 8, 5, 0, 1024>>",
             "achieved": achieved, "peak": PEAK_INT32_TOPS, "unit": "int32 Tops/s",
             "frac": achieved / PEAK_INT32_TOPS, "traffic": pmc_traffic(),
             "kernel_ms": kms,

@@ -709,12 +709,17 @@ static const BaseThresholds &thresholds(uint32_t base) {
     return t;
 }
 
-// Workgroup size per base.  b80's 102 KB mask table leaves room for one
-// workgroup per CU, and the kernel is bound by LDS bank conflicts, so it wants
-// as many waves as fit: 1024 threads (4 waves/SIMD, 128 VGPRs with ~100 bytes
-// of cold spills) run the 1e9 field in 8.49 ms against 8.98 at 768 threads
-// and 9.37 at 512 (scripts/b80_probe.py, profiles/r01/b80_wg_sweep.log).
-#define WG_FOR(b) ((b) == 80 ? 1024 : 512)
+// Workgroup size per base (fields >= 1e7).  The kernels are bound by LDS bank
+// conflicts, so they want as many lookups in flight as fit.  b80's 102 KB
+// mask table leaves room for one workgroup per CU: 1024 threads (4 waves/SIMD,
+// 128 VGPRs with ~100 bytes of cold spills) run the 1e9 field in 8.47 ms
+// against 8.98 at 768 threads and 9.37 at 512 (scripts/b80_probe.py,
+// profiles/r01/b80_wg_sweep.log).  b40: two 1024-thread workgroups per CU
+// (8 waves/SIMD, 64 VGPRs, 16 bytes of spills) 2.38-2.39 ms against 2.43 for
+// three 512-thread ones (6 waves/SIMD) and 2.79 for two 896-thread ones (14
+// waves do not split evenly over 4 SIMDs; profiles/r01/fd2_wg_sweep2.log).
+// b50's tables (60 KB) allow 4 waves/SIMD either way.
+#define WG_FOR(b) ((b) == 50 ? 512 : 1024)
 #define FD2_COMBOS(X)                                                                           \
     X(40, 4, 8, 5) X(40, 5, 8, 5) X(40, 5, 9, 5) X(50, 5, 10, 6) X(50, 6, 10, 6) X(50, 6, 11, 6) \
         X(80, 8, 16, 9) X(80, 9, 16, 9) X(80, 9, 17, 9)
@@ -733,19 +738,19 @@ static hipError_t launch_segment(const DetailedLaunch &p, int num_cus, hipStream
         // (6 waves/SIMD) tie at 2.56-2.58 ms, 1024 (8 waves, spills) 2.59,
         // 896 (7 waves) 2.85-2.92, 640 (5 waves) 3.18.
         if (probe == 6) return launch_cfg<Cfg<40, 4, 8, 5, 0, 768>>(p, num_cus, s);
+        if (probe == 7) return launch_cfg<Cfg<40, 4, 8, 5, 0, 1024>>(p, num_cus, s);
+        if (probe == 5) return launch_cfg<Cfg<40, 4, 8, 5, 0, 896>>(p, num_cus, s);
         if (probe == 8) return launch_cfg<Cfg<40, 4, 8, 5, 0, 512, 1>>(p, num_cus, s);
         if (probe == 9) return launch_cfg<Cfg<40, 4, 8, 5, 0, 512, 2>>(p, num_cus, s);
     }
-    // b80 fields too small to fill the chip keep 512-thread workgroups (the
-    // per-workgroup table build dominates there: 1e6 kernel 30 vs 38 us).
-    if (p.base == 80 && (probe == 20 || p.count < 10000000ull)) {
-        if (c.nd == 8 && c.ne == 16) return launch_cfg<Cfg<80, 8, 16, 9, 0, 512>>(p, num_cus, s);
-        if (c.nd == 9 && c.ne == 16) return launch_cfg<Cfg<80, 9, 16, 9, 0, 512>>(p, num_cus, s);
-        if (c.nd == 9 && c.ne == 17) return launch_cfg<Cfg<80, 9, 17, 9, 0, 512>>(p, num_cus, s);
-    }
-#define X(B_, ND_, NE_, NE2_)                                              \
-    if (p.base == B_ && c.nd == ND_ && c.ne == NE_ && c.ne2 == NE2_)        \
-        return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WG_FOR(B_)>>(p, num_cus, s);
+    // Fields too small to fill the chip keep 512-thread workgroups (the
+    // per-workgroup table build dominates there: b80 1e6 kernel 30 vs 38 us);
+    // probe 20 forces them for b80 comparisons.
+    const bool wg512 = p.count < 10000000ull || (probe == 20 && p.base == 80);
+#define X(B_, ND_, NE_, NE2_)                                                          \
+    if (p.base == B_ && c.nd == ND_ && c.ne == NE_ && c.ne2 == NE2_)                    \
+        return wg512 ? launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512>>(p, num_cus, s)       \
+                     : launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WG_FOR(B_)>>(p, num_cus, s);
     FD2_COMBOS(X)
 #undef X
     return hipErrorInvalidValue;

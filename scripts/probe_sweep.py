@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import nice_amd as N  # noqa: E402
 
-EXACT = {0, 6, 8, 9}
+EXACT = {0, 5, 6, 7, 8, 9}
 ctx = N.GpuContext(0)
 s = N.get_base_range_u128(40).range_start
 probes = [int(x) for x in sys.argv[1:]] or [0, 1, 2, 3, 6, 0]

@@ -9,7 +9,7 @@ import json
 import statistics
 import sys
 
-KERNEL = "fd2::fd2_kernel<nice::fd2::Cfg<40, 4, 8, 5, 0, 512, 0>"
+KERNEL = "fd2::fd2_kernel<nice::fd2::Cfg<40, 4, 8, 5, 0, 1024, 0>"
 
 
 def per_dispatch(path, counter):
