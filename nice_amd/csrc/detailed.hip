@@ -74,9 +74,40 @@ __global__ void unique_counts_kernel(const u64 *n_pairs, u32 count, GenericBase 
     if (i < count) out[i] = unique_generic(n_pairs[2 * i], n_pairs[2 * i + 1], g);
 }
 
+// Field epilogue: sum the kHistCopies histogram copies into `out` (129 bins,
+// then the near-miss count at out[129]) and zero the copies and the counter
+// for the next field.  `out` is mapped pinned host memory, so the host reads
+// the result straight after its completion event: no memset and no DMA copy
+// on the field's critical path.
+__global__ void __launch_bounds__(1024) detailed_finish_kernel(u64 *__restrict__ hist, u32 *__restrict__ count,
+                                                               u64 *__restrict__ out) {
+    __shared__ u64 acc[129];
+    const u32 t = threadIdx.x;
+    if (t < 129) acc[t] = 0;
+    __syncthreads();
+    for (u32 e = t; e < kHistCopies * 129; e += blockDim.x) {
+        const u64 v = hist[e];
+        if (v) {
+            atomicAdd((unsigned long long *)&acc[e % 129], (unsigned long long)v);
+            hist[e] = 0;
+        }
+    }
+    __syncthreads();
+    if (t < 129) out[t] = acc[t];
+    if (t == 129) {
+        out[129] = *count;
+        *count = 0;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------
+hipError_t launch_detailed_finish(uint64_t *hist, uint32_t *count, uint64_t *out_mapped, hipStream_t s) {
+    hipLaunchKernelGGL(detailed_finish_kernel, dim3(1), dim3(1024), 0, s, hist, count, out_mapped);
+    return hipGetLastError();
+}
+
 hipError_t launch_detailed_generic(const DetailedLaunch &p, int num_cus, hipStream_t s) {
     GenericBase g = make_generic(p.base);
     u64 grid = (p.count + 255) / 256;

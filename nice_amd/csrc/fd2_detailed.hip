@@ -746,7 +746,8 @@ static hipError_t launch_segment(const DetailedLaunch &p, int num_cus, hipStream
     // Fields too small to fill the chip keep 512-thread workgroups (the
     // per-workgroup table build dominates there: b80 1e6 kernel 30 vs 38 us);
     // probe 20 forces them for b80 comparisons.
-    const bool wg512 = p.count < 10000000ull || (probe == 20 && p.base == 80);
+    static const bool force512 = getenv("NICE_FD2_WG512") != nullptr;
+    const bool wg512 = force512 || p.count < 10000000ull || (probe == 20 && p.base == 80);
 #define X(B_, ND_, NE_, NE2_)                                                          \
     if (p.base == B_ && c.nd == ND_ && c.ne == NE_ && c.ne2 == NE2_)                    \
         return wg512 ? launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512>>(p, num_cus, s)       \

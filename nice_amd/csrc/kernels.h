@@ -38,6 +38,9 @@ bool fd2_supported(uint32_t base);
 hipError_t launch_detailed_fd2(const DetailedLaunch &p, int num_cus, hipStream_t s);
 // The n where fd2's per-segment limb layout changes (ascending).
 size_t fd2_cuts(uint32_t base, unsigned __int128 *out, size_t cap);
+// Field epilogue on the launch stream: out_mapped[0..128] = the summed
+// histogram copies, out_mapped[129] = *count; copies and counter are zeroed.
+hipError_t launch_detailed_finish(uint64_t *hist, uint32_t *count, uint64_t *out_mapped, hipStream_t s);
 // Generic per-n kernel: any base 2..128, any n < 2^128.
 hipError_t launch_detailed_generic(const DetailedLaunch &p, int num_cus, hipStream_t s);
 

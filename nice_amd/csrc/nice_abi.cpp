@@ -88,6 +88,9 @@ struct Device {
     uint32_t list_cap = 0;
     uint64_t *h_hist = nullptr;   // pinned
     uint32_t *h_count = nullptr;  // pinned
+    uint64_t *h_fin = nullptr;    // mapped pinned: summed histogram [0..128], near-miss count [129]
+    uint64_t *d_fin = nullptr;    // device view of h_fin
+    bool state_dirty = true;      // d_hist / d_count[0] not known to be zero
     std::map<uint32_t, uint32_t *> residues;  // base*8+k -> device residue table
     std::map<uint32_t, uint32_t *> ranks;     // base*8+k -> lower_bound(residues, r), r in [0, M]
     LeafBuf desc[2];
@@ -181,6 +184,8 @@ int device_init(Device &d, int id) {
     d.d_count = (uint32_t *)(d.d_hist + kHistCopies * 129);
     HIPCHK(hipHostMalloc(&d.h_hist, kStateBytes, hipHostMallocDefault));
     d.h_count = (uint32_t *)(d.h_hist + kHistCopies * 129);
+    HIPCHK(hipHostMalloc(&d.h_fin, 130 * 8, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void **)&d.d_fin, d.h_fin, 0));
     int rc = ensure_list(d, kInitialListCap);
     if (rc) return rc;
     return NICE_OK;
@@ -208,6 +213,7 @@ void device_free(Device &d) {
     (void)hipFree(d.d_list_n);
     (void)hipFree(d.d_list_u);
     (void)hipHostFree(d.h_hist);
+    (void)hipHostFree(d.h_fin);
     (void)hipEventDestroy(d.ev0);
     (void)hipEventDestroy(d.ev1);
     (void)hipEventDestroy(d.ev_done);
@@ -368,14 +374,17 @@ int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start
         d.last = nice_kernel_stats{};
         if (bounds[i] >= bounds[i + 1]) continue;
         HIPCHK(hipSetDevice(d.id));
-        HIPCHK(hipMemsetAsync(d.d_hist, 0, kStateBytes, d.stream));
+        // The state block is zeroed by the previous field's epilogue; a
+        // memset only after an interrupted field (or the first one).
+        if (d.state_dirty) HIPCHK(hipMemsetAsync(d.d_hist, 0, kStateBytes, d.stream));
+        d.state_dirty = true;
         HIPCHK(hipEventRecord(d.ev0, d.stream));
         bool used_fd = false;
         uint64_t fdc = 0;
         int rc = enqueue_detailed(d, bounds[i], bounds[i + 1], base, used_fd, fdc);
         if (rc) return rc;
         HIPCHK(hipEventRecord(d.ev1, d.stream));
-        HIPCHK(hipMemcpyAsync(d.h_hist, d.d_hist, kStateBytes, hipMemcpyDeviceToHost, d.stream));
+        HIPCHK(nice::launch_detailed_finish(d.d_hist, d.d_count, d.d_fin, d.stream));
         HIPCHK(hipEventRecord(d.ev_done, d.stream));
         d.last.fd_kernel = used_fd;
         d.last.numbers = (uint64_t)(bounds[i + 1] - bounds[i]);
@@ -388,27 +397,28 @@ int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start
         if (bounds[i] >= bounds[i + 1]) continue;
         HIPCHK(hipSetDevice(d.id));
         HIPCHK(hipEventSynchronize(d.ev_done));
+        d.state_dirty = false;  // the epilogue zeroed the state block
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, d.ev0, d.ev1));
         d.last.kernel_ms = ms;
-        uint32_t cnt = d.h_count[0];
+        uint32_t cnt = (uint32_t)d.h_fin[129];
         if (cnt > d.list_cap) {
             // Near-miss list overflowed (e.g. out-of-range n, SURVEY hazard 9):
             // grow to the exact count and redo this shard.
             int rc = ensure_list(d, cnt);
             if (rc) return rc;
-            HIPCHK(hipMemsetAsync(d.d_hist, 0, kStateBytes, d.stream));
+            d.state_dirty = true;
             bool used_fd = false;
             uint64_t fdc = 0;
             rc = enqueue_detailed(d, bounds[i], bounds[i + 1], base, used_fd, fdc);
             if (rc) return rc;
-            HIPCHK(hipMemcpyAsync(d.h_hist, d.d_hist, kStateBytes, hipMemcpyDeviceToHost, d.stream));
+            HIPCHK(nice::launch_detailed_finish(d.d_hist, d.d_count, d.d_fin, d.stream));
             HIPCHK(hipStreamSynchronize(d.stream));
-            cnt = d.h_count[0];
+            d.state_dirty = false;
+            cnt = (uint32_t)d.h_fin[129];
             if (cnt > d.list_cap) return fail(NICE_ERR_HIP, "near-miss list overflow after resize");
         }
-        for (size_t c = 0; c < kHistCopies; c++)
-            for (uint32_t b = 0; b <= base; b++) total[b] += d.h_hist[c * 129 + b];
+        for (uint32_t b = 0; b <= base; b++) total[b] += d.h_fin[b];
         if (cnt) {
             std::vector<uint64_t> nbuf((size_t)cnt * 2);
             std::vector<uint32_t> ubuf(cnt);
