@@ -671,8 +671,9 @@ static Combo combo_at(uint32_t base, u128 e, const std::vector<Nat> &pw) {
 }
 
 struct BaseThresholds {
-    std::vector<Nat> pw;     // B^k
-    std::vector<u128> cuts;  // n where the combo changes, ascending, inside the range
+    std::vector<Nat> pw;       // B^k
+    std::vector<u128> cuts;    // n where the combo changes, ascending, inside the range
+    std::vector<Combo> combos; // combos[i]: segments ending in (cuts[i-1], cuts[i]]
 };
 
 static const BaseThresholds &thresholds(uint32_t base) {
@@ -689,6 +690,7 @@ static const BaseThresholds &thresholds(uint32_t base) {
     // Walk the range: binary-search each change of combo_at.
     u128 a = rs;
     Combo cur = combo_at(base, a + 1, t.pw);
+    t.combos.push_back(cur);
     while (true) {
         Combo last = combo_at(base, re, t.pw);
         if (last.nd == cur.nd && last.ne == cur.ne && last.ne2 == cur.ne2) break;
@@ -704,6 +706,7 @@ static const BaseThresholds &thresholds(uint32_t base) {
         t.cuts.push_back(lo - 1);
         a = lo - 1;
         cur = combo_at(base, lo, t.pw);
+        t.combos.push_back(cur);
     }
     have[base] = true;
     return t;
@@ -724,10 +727,9 @@ static const BaseThresholds &thresholds(uint32_t base) {
     X(40, 4, 8, 5) X(40, 5, 8, 5) X(40, 5, 9, 5) X(50, 5, 10, 6) X(50, 6, 10, 6) X(50, 6, 11, 6) \
         X(80, 8, 16, 9) X(80, 9, 16, 9) X(80, 9, 17, 9)
 
-static hipError_t launch_segment(const DetailedLaunch &p, int num_cus, hipStream_t s) {
-    const BaseThresholds &t = thresholds(p.base);
-    u128 a = ((u128)p.start_hi << 64) | p.start_lo;
-    const Combo c = combo_at(p.base, a + p.count, t.pw);
+// c: the limb counts of the segment's cut interval (cached in thresholds(),
+// no bignum work per launch).
+static hipError_t launch_segment(const DetailedLaunch &p, const Combo &c, int num_cus, hipStream_t s) {
     const int probe = getenv("NICE_FD2_PROBE") ? atoi(getenv("NICE_FD2_PROBE")) : 0;
     if (probe && p.base == 40 && c.nd == 4 && c.ne == 8 && c.ne2 == 5) {
         if (probe == 1) return launch_cfg<Cfg<40, 4, 8, 5, 1>>(p, num_cus, s);
@@ -782,7 +784,7 @@ hipError_t launch_detailed_fd2(const DetailedLaunch &p, int num_cus, hipStream_t
         q.start_lo = (uint64_t)a;
         q.start_hi = (uint64_t)(a >> 64);
         q.count = (uint64_t)(stop - a);
-        hipError_t err = fd2::launch_segment(q, num_cus, s);
+        hipError_t err = fd2::launch_segment(q, t.combos[i], num_cus, s);
         if (err != hipSuccess) return err;
         a = stop;
     }

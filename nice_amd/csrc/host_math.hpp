@@ -6,6 +6,8 @@
 // against oracle/ and the reference's golden vectors.
 #pragma once
 
+#include <mutex>
+
 #include <stdint.h>
 
 #include <algorithm>
@@ -129,6 +131,23 @@ inline int base_range(uint32_t b, u128 &start, u128 &end) {
     }
     if (!ok) return -1;
     return start < end ? 1 : 0;
+}
+
+// base_range, computed once per base (the bignum roots cost ~13 us, which is
+// a third of a 1e6 field's wall time if paid per call).
+inline int base_range_cached(uint32_t b, u128 &start, u128 &end) {
+    struct Slot {
+        std::once_flag once;
+        int rc = 0;
+        u128 s = 0, e = 0;
+    };
+    static Slot slots[129];
+    if (b > 128) return base_range(b, start, end);
+    Slot &sl = slots[b];
+    std::call_once(sl.once, [&] { sl.rc = base_range(b, sl.s, sl.e); });
+    start = sl.s;
+    end = sl.e;
+    return sl.rc;
 }
 
 // common/src/number_stats.rs:15-17 (f32 arithmetic, as the reference).

@@ -280,7 +280,7 @@ int enqueue_detailed(Device &d, u128 s, u128 e, uint32_t base, bool &used_fd, ui
         return NICE_OK;
     };
     u128 rs = 0, re = 0;
-    const bool fd = nice::fd_supported(base) && nice::base_range(base, rs, re) == 1;
+    const bool fd = nice::fd_supported(base) && nice::base_range_cached(base, rs, re) == 1;
     if (!fd) return launch(s, e, false);
     int rc;
     if ((rc = launch(s, std::min(e, rs), false))) return rc;
@@ -333,7 +333,7 @@ void nice_ctx_destroy(nice_ctx *ctx) {
 
 int nice_base_range(uint32_t base, uint64_t *slo, uint64_t *shi, uint64_t *elo, uint64_t *ehi) {
     u128 s = 0, e = 0;
-    int rc = nice::base_range(base, s, e);
+    int rc = nice::base_range_cached(base, s, e);
     if (rc == 1) {
         *slo = lo64(s);
         *shi = hi64(s);
@@ -477,7 +477,7 @@ int nice_debug_is_nice(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t count, u
 int nice_check_is_nice_inrange(uint32_t base, uint64_t lo, uint64_t hi) {
     u128 rs, re;
     const u128 n = mk(lo, hi);
-    if (!nice::fd2_supported(base) || nice::base_range(base, rs, re) != 1 || n < rs || n >= re)
+    if (!nice::fd2_supported(base) || nice::base_range_cached(base, rs, re) != 1 || n < rs || n >= re)
         return fail(NICE_ERR_INVALID, "n outside the base's valid range (or base not 40/50/80)");
     switch (base) {
     case 40: return nice::is_nice_fast<40>(lo, hi) ? 1 : 0;
@@ -490,7 +490,7 @@ int nice_check_msd_skippable_inrange(uint32_t base, uint64_t slo, uint64_t shi, 
                                      uint64_t ehi) {
     u128 rs, re;
     const u128 s = mk(slo, shi), e = mk(elo, ehi);
-    if (!nice::fd2_supported(base) || nice::base_range(base, rs, re) != 1 || s < rs || e > re || s >= e)
+    if (!nice::fd2_supported(base) || nice::base_range_cached(base, rs, re) != 1 || s < rs || e > re || s >= e)
         return fail(NICE_ERR_INVALID, "range outside the base's valid range (or base not 40/50/80)");
     if (e - s == 1) return 0;  // a single number is never skipped (msd_prefix_filter.rs:395)
     const u128 l = e - 1;
@@ -575,7 +575,7 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
     // Whole field inside the base's valid range: the kernels take their
     // fixed-digit-count fast paths (radix_fast.hpp).
     u128 vr_s = 0, vr_e = 0;
-    const uint32_t in_range = nice::base_range(base, vr_s, vr_e) == 1 && vr_s <= s && e <= vr_e ? 1u : 0u;
+    const uint32_t in_range = nice::base_range_cached(base, vr_s, vr_e) == 1 && vr_s <= s && e <= vr_e ? 1u : 0u;
     const uint32_t R = (uint32_t)table->residues.size();
     const uint64_t M = table->modulus;
     if (M > 0xffffffffull) return fail(NICE_ERR_INVALID, "stride modulus exceeds u32");
