@@ -82,6 +82,8 @@ struct Cfg {
     static constexpr int SH = T + ilog2(ES);                     // carry bit of a scaled limb
     static constexpr u32 ESB = ES * B, EBT = ES * BT;
     static constexpr int WG = WG_;
+    // Target chunk (numbers per lane), see launch_cfg.
+    static constexpr int TCHUNK = BASE == 40 ? 80 : (BASE == 50 ? 160 : 240);
     static constexpr int NBINS = BASE + 1;
     // Histogram window [W0, W0 + W): per-thread counters (u32, or u16 halves
     // shared by threads t and t + WG/2 when LDS is tight).
@@ -566,50 +568,52 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
     if (per_cu_q < 0) return hipErrorInvalidDeviceFunction;
     const int per_cu = per_cu_q < 1 ? 1 : per_cu_q;
     hipError_t e = hipSuccess;
+    // Resident lanes (one "round" of workgroups).
     const u64 lanes = (u64)num_cus * per_cu * P::WG;
     // u16 counters: at most 65535 numbers per lane per launch.
     const u64 max_count = P::HP ? lanes * 60000ull : ~0ull;
     // Every near-miss count must lie above the window (it is recorded on the
     // out-of-window branch).
     if (p.cutoff + 1 < (u32)(P::W0 + P::W)) return hipErrorInvalidValue;
+    // Target numbers per lane.  Short chunks put a wave's 64 lanes on nearby n,
+    // so the top stepped limbs (and the cached ones) of neighbouring lanes are
+    // equal or close and their lookups stop conflicting; a chunk still pays
+    // one init (radix-B conversion and products, ~10 steps).  Each lane takes
+    // one chunk and the grid is many rounds of workgroups, not a persistent
+    // grid: workgroups at different phases (table build, init, steps) share a
+    // CU.  b40 1e9: 2.49 ms persistent at chunk 637, 2.31 persistent at ~80,
+    // 2.19-2.21 at 60-120 non-persistent (scripts/gridx_probe.sh,
+    // profiles/r01/fd2_chunk_sweep.log).
+    static const u64 tchunk_env = getenv("NICE_FD2_TCHUNK") ? strtoull(getenv("NICE_FD2_TCHUNK"), 0, 10) : 0;
+    const u64 tchunk = tchunk_env ? tchunk_env : (u64)P::TCHUNK;
     DetailedLaunch q = p;
     u64 left = p.count;
     while (left) {
         const u64 cnt = left < max_count ? left : max_count;
-        // Chunks of <= B numbers (low-digit table), about 3 per lane, and never
-        // more units than lanes x units-per-lane: a lane with one unit more
-        // than the rest runs alone at the end (989 such units on the b40 1e9
-        // field once cost ~7 % of the launch).
-        const u64 per_lane = (cnt + lanes - 1) / lanes;
-        const u64 upl_min = getenv("NICE_FD2_UPL") ? strtoull(getenv("NICE_FD2_UPL"), 0, 10) : 3;
         // Chunk floor for fields too small to fill the chip: a lane's init
         // costs about ten steps, but with idle CUs latency wins (b40 1e6:
         // kernel 25 us at a floor of 32, 14 us at 4; scripts/small_fields.py).
         const u64 min_chunk = getenv("NICE_FD2_MINCHUNK") ? strtoull(getenv("NICE_FD2_MINCHUNK"), 0, 10) : 4;
-        u64 upl = (per_lane + P::B - 1) / P::B < upl_min ? upl_min : (per_lane + P::B - 1) / P::B;
-        u64 chunk;
-        for (;; upl++) {
-            chunk = (cnt + lanes * upl - 1) / (lanes * upl);  // ceil: cnt / chunk <= lanes * upl
-            // Small fields: at least min_chunk numbers per lane (see above).
-            if (chunk < min_chunk) chunk = cnt < min_chunk ? cnt : min_chunk;
-            if (chunk < 1) chunk = 1;
-            // Odd chunks: lane l of a wave then sits at n mod B = r0 + chunk * l,
-            // so its low-digit entries fall on 32 distinct bank pairs per
-            // half-wave (B is a multiple of 32 for the LSD bases).  Without a
-            // low-digit table (b80) limb 0 of n^2 and n^3 is looked up in the
-            // pair table, and a chunk divisible by 16 puts a 16-lane group on
-            // ONE bank quad for those lookups (n^2 mod 16 equal on every lane):
-            // b80 1e9 at chunk 2544 took 11.8 ms, at 2545 9.3.  Rounding UP
-            // keeps the unit count within lanes x upl.
-            if (chunk > 1 && chunk % 2 == 0) chunk++;
-            if (chunk <= P::B) break;
-        }
+        // Whole rounds of workgroups, chunks <= the target (and <= B, the
+        // low-digit table's reach).
+        u64 rounds = (cnt + tchunk * lanes - 1) / (tchunk * lanes);
+        if (rounds < 1) rounds = 1;
+        u64 chunk = (cnt + rounds * lanes - 1) / (rounds * lanes);
+        if (chunk < min_chunk) chunk = cnt < min_chunk ? cnt : min_chunk;
+        if (chunk < 1) chunk = 1;
+        // Odd chunks: lane l of a wave then sits at n mod B = r0 + chunk * l,
+        // so its low-digit entries fall on 32 distinct bank pairs per
+        // half-wave (B is a multiple of 32 for the LSD bases).  Without a
+        // low-digit table (b80) limb 0 of n^2 and n^3 is looked up in the
+        // pair table, and a chunk divisible by 16 puts a 16-lane group on
+        // ONE bank quad for those lookups (n^2 mod 16 equal on every lane):
+        // b80 1e9 at chunk 2544 took 11.8 ms, at 2545 9.3.
+        if (chunk > 1 && chunk % 2 == 0) chunk++;
+        if (chunk > P::B) chunk = P::B % 2 ? P::B : P::B - 1;
         u64 nunits = cnt / chunk;
         if (nunits > 0xffffffffull) return hipErrorInvalidValue;
         if (nunits) {
-            u64 grid = (nunits + P::WG - 1) / P::WG;
-            const u64 max_grid = (u64)num_cus * per_cu;
-            if (grid > max_grid) grid = max_grid;
+            const u64 grid = (nunits + P::WG - 1) / P::WG;  // one chunk per lane
             hipLaunchKernelGGL(kern, dim3((u32)grid), dim3(P::WG), 0, s, q.start_lo,
                                q.start_hi, (u32)nunits, (u32)chunk, q.cutoff, q.hist, q.out);
             if ((e = hipGetLastError()) != hipSuccess) return e;
