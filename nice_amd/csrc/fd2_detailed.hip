@@ -39,6 +39,7 @@
 // DESIGN.md §3.1 for the cycle model and the measured roofline.
 #include <stdlib.h>
 
+#include <map>
 #include <mutex>
 
 #include "host_math.hpp"
@@ -97,6 +98,7 @@ struct Cfg {
     static constexpr bool LSD = MW <= 2;
     static constexpr int TL = TB + (int)(B * ES);                // low-digit table (2B entries)
     static constexpr int LDS_BYTES = TL + (LSD ? (int)(2 * B * ES) : 0);
+    static constexpr int TAB_BYTES = LDS_BYTES - TB;  // table image copied in per workgroup
     static constexpr int LO = LSD ? 1 : 0;  // first stored / looked-up limb
     // Low-digit entry, word 1: digit bits [0, DB), then the carries and flags
     // of the step n -> n+1, all functions of n mod B (limb 0 of S, C, D1, N3
@@ -136,6 +138,7 @@ struct Cfg {
     static_assert(S_TOPD >= 1 && C_TOPD >= 1, "top limb");
     static_assert(TB >= (int)EBT && TB - (int)EBT < 65536 && (!LSD || TL < 65536), "LDS offsets");
     static_assert(LDS_BYTES <= 163840, "LDS");
+    static_assert(TB % 16 == 0 && TAB_BYTES % 16 == 0, "16-byte table copy");
     static_assert(W0 + W <= NBINS, "window");
     static_assert(!LSD || (ES == 8 && DB > 0 && FC + 6 <= 30), "low-digit entry layout");
     static_assert(C1 || ((unsigned long long)MAGICB * B - (1ull << 32)) * (TMAX / ES) < (1ull << 32),
@@ -410,9 +413,70 @@ __device__ __forceinline__ void step(State<P> &st, const unsigned char *smem, u3
     }
 }
 
+// Table image (the LDS bytes from TB on): digit-pair table, entry e = d1*b +
+// d0 marks d0 and d1; low-digit table (LSD bases), entry r < 2B marks the two
+// low digits of r^2 and of r^3 (mod B) plus the limb-0 carries and wraps.
+template <class P>
+__global__ void fd2_tables_kernel(unsigned char *tb) {
+    const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= P::B) return;
+    u32 v[4] = {0, 0, 0, 0};
+    auto mark = [&](u32 x) {
+        u32 d0 = x % P::BASE, d1 = x / P::BASE;
+        v[d0 >> 5] |= 1u << (d0 & 31);
+        v[d1 >> 5] |= 1u << (d1 & 31);
+    };
+    auto put = [&](unsigned char *p) {
+        if constexpr (P::ES == 4) *(u32 *)p = v[0];
+        else if constexpr (P::ES == 8) *(uint2 *)p = make_uint2(v[0], v[1]);
+        else *(uint4 *)p = make_uint4(v[0], v[1], v[2], v[3]);
+    };
+    mark(e);
+    put(tb + e * P::ES);
+    if constexpr (P::LSD) {
+        v[0] = v[1] = v[2] = v[3] = 0;
+        const u32 B = P::B;
+        const u32 s0 = (u32)((u64)e * e % B), c0 = (u32)((u64)s0 * e % B);
+        mark(s0);
+        mark(c0);
+        const u32 d1 = (2 * e + 1) % B, n3 = (3 * e + 1) % B;
+        v[1] |= d1 + 2 >= B ? P::FLAG_D1 : 0u;                   // D1 limb-0 wrap
+        v[1] |= n3 + 3 >= B ? P::FLAG_N3 : 0u;                   // N3 limb-0 wrap
+        v[1] |= (s0 + d1 >= B ? 8u : 0u) << P::F0;               // S  += D1 carry
+        v[1] |= (P::ES * ((c0 + 3 * s0 + n3) / B)) << P::FC;      // C += 3S + N3 carry
+        put(tb + (P::TL - P::TB) + e * P::ES);
+        put(tb + (P::TL - P::TB) + (e + P::B) * P::ES);
+    }
+}
+
+// The table image for this device and base, built on first use (the layout
+// depends on the base only) and kept for the process.
+template <class P>
+static hipError_t fd2_tables(hipStream_t s, const uint4 **out) {
+    static std::mutex mu;
+    static std::map<int, unsigned char *> have;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = have.find(dev);
+    if (it == have.end()) {
+        unsigned char *t = nullptr;
+        if ((e = hipMalloc(&t, P::TAB_BYTES)) != hipSuccess) return e;
+        hipLaunchKernelGGL(fd2_tables_kernel<P>, dim3((P::B + 255) / 256), dim3(256), 0, s, t);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        // other streams (contexts) of this device may read it next
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        it = have.emplace(dev, t).first;
+    }
+    *out = (const uint4 *)it->second;
+    return hipSuccess;
+}
+
 template <class P>
 __device__ __forceinline__ void fd2_body(u64 start_lo, u64 start_hi, u32 nunits, u32 chunk, u32 cutoff,
-                                         u64 *__restrict__ hist_out, NumOut out) {
+                                         u64 *__restrict__ hist_out, NumOut out,
+                                         const uint4 *__restrict__ tabs) {
     // Static LDS: its address is a compile-time constant, so a lookup is one
     // ds_read with the table offset in the instruction's immediate field.
     __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDS_BYTES];
@@ -420,38 +484,15 @@ __device__ __forceinline__ void fd2_body(u64 start_lo, u64 start_hi, u32 nunits,
     u32 *outl = (u32 *)(smem + P::OUTL);
     const u32 tid = threadIdx.x;
 
-    // Digit-pair table: entry e = d1*b + d0 marks d0 and d1.  Low-digit table:
-    // entry r (< 2B) marks the two low digits of r^2 and of r^3 (mod B).
-    for (u32 e = tid; e < P::B; e += P::WG) {
-        u32 v[4] = {0, 0, 0, 0};
-        auto mark = [&](u32 x) {
-            u32 d0 = x % P::BASE, d1 = x / P::BASE;
-            v[d0 >> 5] |= 1u << (d0 & 31);
-            v[d1 >> 5] |= 1u << (d1 & 31);
-        };
-        auto put = [&](unsigned char *p) {
-            if constexpr (P::ES == 4) *(u32 *)p = v[0];
-            else if constexpr (P::ES == 8) *(uint2 *)p = make_uint2(v[0], v[1]);
-            else *(uint4 *)p = make_uint4(v[0], v[1], v[2], v[3]);
-        };
-        mark(e);
-        put(smem + P::TB + e * P::ES);
-        if constexpr (P::LSD) {
-            v[0] = v[1] = v[2] = v[3] = 0;
-            const u32 B = P::B;
-            const u32 s0 = (u32)((u64)e * e % B), c0 = (u32)((u64)s0 * e % B);
-            mark(s0);
-            mark(c0);
-            const u32 d1 = (2 * e + 1) % B, n3 = (3 * e + 1) % B;
-            v[1] |= d1 + 2 >= B ? P::FLAG_D1 : 0u;                   // D1 limb-0 wrap
-            v[1] |= n3 + 3 >= B ? P::FLAG_N3 : 0u;                   // N3 limb-0 wrap
-            v[1] |= (s0 + d1 >= B ? 8u : 0u) << P::F0;               // S  += D1 carry
-            v[1] |= (P::ES * ((c0 + 3 * s0 + n3) / B)) << P::FC;      // C += 3S + N3 carry
-            put(smem + P::TL + e * P::ES);
-            put(smem + P::TL + (e + P::B) * P::ES);
-        }
+    // The tables (built once per device and base in global memory,
+    // fd2_tables) are copied in with 16-byte accesses, and the histogram
+    // region zeroed: building them here cost ~5 % of a launch of short chunks.
+    {
+        uint4 *dst = (uint4 *)(smem + P::TB);
+        for (u32 i = tid; i < (u32)(P::TAB_BYTES / 16); i += P::WG) dst[i] = tabs[i];
+        uint4 *h4 = (uint4 *)smem;
+        for (u32 i = tid; i < (u32)(P::TB / 16); i += P::WG) h4[i] = make_uint4(0, 0, 0, 0);
     }
-    for (u32 i = tid; i < (u32)(P::TB / 4); i += P::WG) hist[i] = 0;
     __syncthreads();
 
     // Window counters: row u - W0, column tid (u32) or tid mod WG/2 (u16 half).
@@ -545,14 +586,14 @@ __device__ __forceinline__ void fd2_body(u64 start_lo, u64 start_hi, u32 nunits,
 template <class P>
 __global__ void __launch_bounds__(P::WG) __attribute__((amdgpu_waves_per_eu(P::WPE, P::WPE)))
 fd2_kernel(u64 start_lo, u64 start_hi, u32 nunits, u32 chunk, u32 cutoff, u64 *__restrict__ hist_out,
-           NumOut out) {
-    fd2_body<P>(start_lo, start_hi, nunits, chunk, cutoff, hist_out, out);
+           NumOut out, const uint4 *__restrict__ tabs) {
+    fd2_body<P>(start_lo, start_hi, nunits, chunk, cutoff, hist_out, out, tabs);
 }
 template <class P>
 __global__ void __launch_bounds__(P::WG) __attribute__((amdgpu_waves_per_eu(P::WPE, P::WPE)))
 fd2_tail_kernel(u64 start_lo, u64 start_hi, u32 nunits, u32 cutoff, u64 *__restrict__ hist_out,
-                NumOut out) {
-    fd2_body<P>(start_lo, start_hi, nunits, 1u, cutoff, hist_out, out);
+                NumOut out, const uint4 *__restrict__ tabs) {
+    fd2_body<P>(start_lo, start_hi, nunits, 1u, cutoff, hist_out, out, tabs);
 }
 
 template <class P>
@@ -586,6 +627,8 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
     // profiles/r01/fd2_chunk_sweep.log).
     static const u64 tchunk_env = getenv("NICE_FD2_TCHUNK") ? strtoull(getenv("NICE_FD2_TCHUNK"), 0, 10) : 0;
     const u64 tchunk = tchunk_env ? tchunk_env : (u64)P::TCHUNK;
+    const uint4 *tabs = nullptr;
+    if ((e = fd2_tables<P>(s, &tabs)) != hipSuccess) return e;
     DetailedLaunch q = p;
     u64 left = p.count;
     while (left) {
@@ -615,7 +658,7 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         if (nunits) {
             const u64 grid = (nunits + P::WG - 1) / P::WG;  // one chunk per lane
             hipLaunchKernelGGL(kern, dim3((u32)grid), dim3(P::WG), 0, s, q.start_lo,
-                               q.start_hi, (u32)nunits, (u32)chunk, q.cutoff, q.hist, q.out);
+                               q.start_hi, (u32)nunits, (u32)chunk, q.cutoff, q.hist, q.out, tabs);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
         const u64 tail = cnt - nunits * chunk;  // < chunk <= B: one number per lane
@@ -623,7 +666,7 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
             u64 lo = q.start_lo, hi = q.start_hi;
             add_u128(lo, hi, nunits * chunk);
             hipLaunchKernelGGL(fd2_tail_kernel<P>, dim3((u32)((tail + P::WG - 1) / P::WG)), dim3(P::WG), 0,
-                               s, lo, hi, (u32)tail, q.cutoff, q.hist, q.out);
+                               s, lo, hi, (u32)tail, q.cutoff, q.hist, q.out, tabs);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
         add_u128(q.start_lo, q.start_hi, cnt);
