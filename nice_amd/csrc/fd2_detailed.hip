@@ -41,6 +41,7 @@
 
 #include <map>
 #include <mutex>
+#include <type_traits>
 
 #include "host_math.hpp"
 #include "kernels.h"
@@ -227,7 +228,7 @@ __device__ __forceinline__ void recompute_hi(State<P> &st, const unsigned char *
 // Radix-B normalisation of u64 column sums into M limbs (the value fits by the
 // host's choice of limb counts; a carry past limb M-1 is dropped).
 template <class P, int N, int M>
-__device__ __forceinline__ void normalize(const u64 (&acc)[N], u32 (&out)[M]) {
+__device__ __forceinline__ void normalize64(const u64 (&acc)[N], u32 (&out)[M]) {
     u64 cy = 0;
 #pragma unroll
     for (int t = 0; t < M; t++) {
@@ -237,54 +238,125 @@ __device__ __forceinline__ void normalize(const u64 (&acc)[N], u32 (&out)[M]) {
     }
 }
 
+// Radix-B normalisation of column sums into M limbs (the value fits by the
+// host's choice of limb counts; a carry past limb M-1 is dropped).  A is u32
+// where every column sum fits 32 bits (static_assert in init), else u64.
+template <class P, class A, int N, int M>
+__device__ __forceinline__ void normalize(const A (&acc)[N], u32 (&out)[M]) {
+    A cy = 0;
+#pragma unroll
+    for (int t = 0; t < M; t++) {
+        const A v = (t < N ? acc[t] : (A)0) + cy;
+        cy = v / P::B;
+        out[t] = (u32)(v - cy * P::B);
+    }
+}
+
 template <class P>
 __device__ __forceinline__ void init(State<P> &st, u64 n_lo, u64 n_hi, const unsigned char *smem) {
     constexpr u32 B = P::B;
-    u32 w[4] = {(u32)n_lo, (u32)(n_lo >> 32), (u32)n_hi, (u32)(n_hi >> 32)};
     u32 X[P::NX];
+    if constexpr (P::BASE != 80) {
+        // In-range n fits 64 bits (b40 < 2^43, b50 < 2^57): two radix-B digits
+        // per u64 division by B^2, the rest in 32 bits.
+        (void)n_hi;
+        constexpr u64 B2 = (u64)B * B;
+        u64 v = n_lo;
 #pragma unroll
-    for (int j = 0; j < P::NX; j++) {
-        u64 rem = 0;
-#pragma unroll
-        for (int q = 3; q >= 0; q--) {
-            u64 cur = (rem << 32) | w[q];
-            w[q] = (u32)(cur / B);
-            rem = cur % B;
+        for (int j = 0; j < P::NX; j += 2) {
+            const u64 q = v / B2;
+            const u32 r = (u32)(v - q * B2);
+            X[j] = r % B;
+            if (j + 1 < P::NX) X[j + 1] = r / B;
+            v = q;
         }
-        X[j] = (u32)rem;
+    } else {
+        u32 w[4] = {(u32)n_lo, (u32)(n_lo >> 32), (u32)n_hi, (u32)(n_hi >> 32)};
+#pragma unroll
+        for (int j = 0; j < P::NX; j++) {
+            u64 rem = 0;
+#pragma unroll
+            for (int q = 3; q >= 0; q--) {
+                u64 cur = (rem << 32) | w[q];
+                w[q] = (u32)(cur / B);
+                rem = cur % B;
+            }
+            X[j] = (u32)rem;
+        }
     }
-    st.r8 = X[0] * P::ES;
-    {  // S = X^2
-        u64 acc[2 * P::NX];
+    // Column sums: at most min(NS, NX) products < B^2 plus a carry: 32 bits.
+    static_assert((unsigned long long)P::NX * B * B + 2ull * B < (1ull << 32), "32-bit init columns");
+    using A = u32;
+    if constexpr (P::BASE == 80) {
+        // b80 (1024-thread kernel at the 128-VGPR cap): u64 columns, the
+        // layout whose register allocation spills least.
+        st.r8 = X[0] * P::ES;
+        {
+            u64 acc[2 * P::NX];
 #pragma unroll
-        for (int t = 0; t < 2 * P::NX; t++) acc[t] = 0;
+            for (int t = 0; t < 2 * P::NX; t++) acc[t] = 0;
 #pragma unroll
-        for (int i = 0; i < P::NX; i++)
+            for (int i = 0; i < P::NX; i++)
 #pragma unroll
-            for (int j = 0; j < P::NX; j++) acc[i + j] += (u64)X[i] * X[j];
-        normalize<P>(acc, st.S);
-    }
-    {  // C = S * X
-        u64 acc[P::NS + P::NX];
+                for (int j = 0; j < P::NX; j++) acc[i + j] += (u64)X[i] * X[j];
+            normalize64<P>(acc, st.S);
+        }
+        {
+            u64 acc[P::NS + P::NX];
 #pragma unroll
-        for (int t = 0; t < P::NS + P::NX; t++) acc[t] = 0;
+            for (int t = 0; t < P::NS + P::NX; t++) acc[t] = 0;
 #pragma unroll
-        for (int i = 0; i < P::NS; i++)
+            for (int i = 0; i < P::NS; i++)
 #pragma unroll
-            for (int j = 0; j < P::NX; j++) acc[i + j] += (u64)st.S[i] * X[j];
-        normalize<P>(acc, st.C);
-    }
-    {  // D1 = 2n + 1
-        u64 acc[P::NX];
+                for (int j = 0; j < P::NX; j++) acc[i + j] += (u64)st.S[i] * X[j];
+            normalize64<P>(acc, st.C);
+        }
+        {
+            u64 acc[P::NX];
 #pragma unroll
-        for (int t = 0; t < P::NX; t++) acc[t] = 2ull * X[t] + (t == 0 ? 1 : 0);
-        normalize<P>(acc, st.D1);
-    }
-    {  // N3 = 3n + 1
-        u64 acc[P::NX];
+            for (int t = 0; t < P::NX; t++) acc[t] = 2ull * X[t] + (t == 0 ? 1 : 0);
+            normalize64<P>(acc, st.D1);
+        }
+        {
+            u64 acc[P::NX];
 #pragma unroll
-        for (int t = 0; t < P::NX; t++) acc[t] = 3ull * X[t] + (t == 0 ? 1 : 0);
-        normalize<P>(acc, st.N3);
+            for (int t = 0; t < P::NX; t++) acc[t] = 3ull * X[t] + (t == 0 ? 1 : 0);
+            normalize64<P>(acc, st.N3);
+        }
+    } else {
+        st.r8 = X[0] * P::ES;
+        {  // S = X^2
+            A acc[2 * P::NX];
+#pragma unroll
+            for (int t = 0; t < 2 * P::NX; t++) acc[t] = 0;
+#pragma unroll
+            for (int i = 0; i < P::NX; i++)
+#pragma unroll
+                for (int j = 0; j < P::NX; j++) acc[i + j] += (A)X[i] * X[j];
+            normalize<P>(acc, st.S);
+        }
+        {  // C = S * X
+            A acc[P::NS + P::NX];
+#pragma unroll
+            for (int t = 0; t < P::NS + P::NX; t++) acc[t] = 0;
+#pragma unroll
+            for (int i = 0; i < P::NS; i++)
+#pragma unroll
+                for (int j = 0; j < P::NX; j++) acc[i + j] += (A)st.S[i] * X[j];
+            normalize<P>(acc, st.C);
+        }
+        {  // D1 = 2n + 1
+            A acc[P::NX];
+#pragma unroll
+            for (int t = 0; t < P::NX; t++) acc[t] = 2 * (A)X[t] + (t == 0 ? 1 : 0);
+            normalize<P>(acc, st.D1);
+        }
+        {  // N3 = 3n + 1
+            A acc[P::NX];
+#pragma unroll
+            for (int t = 0; t < P::NX; t++) acc[t] = 3 * (A)X[t] + (t == 0 ? 1 : 0);
+            normalize<P>(acc, st.N3);
+        }
     }
     recompute_hi<P>(st, smem);
     if constexpr (P::LSD) st.S[0] = st.C[0] = st.D1[0] = st.N3[0] = 0;  // from the table
