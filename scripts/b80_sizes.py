@@ -26,6 +26,4 @@ for n in (5e7, 1e8, 2e8, 4e8, 6e8, 8e8, 1e9):
     print(f"b{base} {n:.0e}: {t:.3f} ms  {t / n * 1e9:.3f} ms per 1e9", flush=True)
 tot = sum(kern(s + i * 2 * 10 ** 8, 2 * 10 ** 8) for i in range(5))
 print(f"b{base} 1e9 as 5 x 2e8: {tot:.3f} ms", flush=True)
-for upl in (3, 6, 15, 30):
-    os.environ["NICE_FD2_UPL"] = str(upl)
-    print(f"b{base} 1e9 upl>={upl}: {kern(s, 10 ** 9):.3f} ms", flush=True)
+# (the chunk-length sweep is scripts/gridx_probe.sh, NICE_FD2_TCHUNK)
