@@ -1,13 +1,12 @@
-# Bench-step A/B (alternating, 20 steps each, no CPU baseline): host wait mode
-# (NICE_BLOCKING_SYNC=1 vs spin) and detailed workgroup size (NICE_FD2_WG512=1
-# vs the 1024-thread default), printed as ms/step, both-modes wall median and
-# detailed kernel ms.
+# Bench-step A/B (alternating, 20 steps each, no CPU baseline): detailed
+# workgroup size (NICE_FD2_WG512=1 vs the 1024-thread default) and the two
+# modes at once vs in sequence (--sequential), printed as ms/step, both-modes
+# wall median and detailed kernel ms.
 set -e
 cd /root/repo
 for i in 1 2; do
   NICE_FD2_WG512=1 timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/ab_wg512_$i.json
-  timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/ab_spin_$i.json
-  NICE_BLOCKING_SYNC=1 timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/ab_block_$i.json
+  timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/ab_default_$i.json
   timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 --sequential > gpurun_out/ab_seq_$i.json
 done
 for f in gpurun_out/ab_*.json; do
