@@ -447,6 +447,10 @@ __device__ __forceinline__ void step(State<P> &st, const unsigned char *smem, u3
 #pragma unroll
     for (int i = L0; i < CT; i++) {
         u32 t = st.C[i] + cC;
+        // Past limb L0 the carry is c * ES from a multiply-high: keep C + c*ES
+        // one v_lshl_add_u32 and add N3 with a plain v_add_u32 (LLVM would
+        // otherwise emit v_lshlrev_b32 + v_add3_u32, ~2 issue cycles more).
+        if (i > L0 && i < P::NN) asm("" : "+v"(t));
         if (i < P::NN) t += st.N3[i];
         else if (i < P::SL) t -= 3 * P::EBT;
         // + 3S as one v_mad_u32_u24 (limbs < 2^24)
