@@ -80,6 +80,8 @@ def _gather_rows(rows: Sequence[Tuple[int, int]], dist, group,
     """all_gather of variable-length (number, aux) lists, in rank order.  With
     `counts` (every rank's list length, already exchanged) no count collective
     is issued, and nothing at all when every list is empty."""
+    if counts is not None and not any(counts):
+        return []  # every list empty (the usual case): no collective, no device work
     import torch
     dev = _device(dist, group)
     world = dist.get_world_size(group)
