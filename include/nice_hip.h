@@ -65,13 +65,23 @@ int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start
 
 /* Niceonly tuning (all zero = reference CPU-path semantics, which make the
  * candidate set identical to process_range_niceonly's):
- *   msd_floor  MSD recursion floor; 0 -> 250 (msd_prefix_filter.rs:282)
+ *   msd_floor  MSD recursion floor; 0 -> NICE_GPU_MSD_FLOOR from the
+ *              environment when set to a number >= 1 (the reference's pin,
+ *              client_process_gpu.rs:161-172), else 250 (msd_prefix_filter.rs:282)
  *   chunk_size MSD chunking of the field; 0 -> reference client rule
  *              1e6 * clamp(ceil(size / 1e11), 1, 1000) (client/src/main.rs:158-168)
  *   threads    host MSD worker threads; 0 -> hardware concurrency
  *   stride_k   LSD digits in the stride table; 0 -> 2 (client/src/main.rs:19)
  *   msd_where  where the MSD recursion runs: 0 auto (device for stride_k 2),
  *              1 host worker threads, 2 device (level-synchronous kernels)
+ *   deal_stride, deal_offset
+ *              process only the field's chunks c with c % deal_stride ==
+ *              deal_offset (0 / 0 -> every chunk).  Rank r of an N-way job
+ *              passes (N, r) with the whole field's bounds: the chunk grid and
+ *              hence every chunk's MSD ranges are those of the single-process
+ *              run, and survival skew along the field is spread over ranks (the
+ *              reference deals descriptors from a shared channel,
+ *              client_process_gpu.rs:589-709).
  * Both MSD placements produce the same candidate set. */
 #define NICE_MSD_AUTO 0
 #define NICE_MSD_HOST 1
@@ -82,11 +92,13 @@ typedef struct {
     int32_t threads;
     uint32_t stride_k;
     int32_t msd_where;
+    uint32_t deal_stride;
+    uint32_t deal_offset;
     uint32_t reserved;
 } nice_niceonly_opts;
 
 typedef struct {
-    uint64_t ranges;        /* MSD-surviving sub-ranges */
+    uint64_t ranges;        /* MSD-surviving sub-ranges (get_valid_ranges output) */
     uint64_t range_numbers; /* numbers inside them */
     uint64_t candidates;    /* stride candidates checked on the GPU */
     uint32_t launches;
@@ -106,6 +118,17 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
                                    uint64_t end_lo, uint64_t end_hi, uint32_t base,
                                    const nice_niceonly_opts *opts, nice_number *out,
                                    size_t cap, size_t *n_out, nice_niceonly_stats *stats);
+
+/* The coordination server's submit checks for a detailed result
+ * (api/src/main.rs:309-359), which nice_process_range_detailed also applies to
+ * its own output before returning (plus the server's recompute of every listed
+ * number, on the device): the histogram (base+1 bins) sums to the field size
+ * (size_lo, size_hi); every listed number lies above the near-miss cutoff; for
+ * each bin above the cutoff the count equals the number of listed entries with
+ * that num_uniques; the list length equals the sum of those bins.
+ * NICE_OK or NICE_ERR_INVALID with the failed check in nice_last_error(). */
+int nice_validate_detailed(uint32_t base, uint64_t size_lo, uint64_t size_hi, const uint64_t *hist,
+                           const nice_number *list, size_t n);
 
 /* Device time of the hot kernel(s) in the last detailed call on a device,
  * measured with HIP events on the launch stream. */

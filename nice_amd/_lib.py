@@ -28,7 +28,7 @@ EXPORTS = (
     "nice_gpu_supports_base", "nice_fd_kernel_base", "nice_msd_valid_ranges",
     "nice_msd_skippable", "nice_stride_table", "nice_debug_unique_counts",
     "nice_debug_is_nice", "nice_check_is_nice_inrange", "nice_check_msd_skippable_inrange",
-    "nice_fd_segment_cuts",
+    "nice_fd_segment_cuts", "nice_validate_detailed",
 )
 
 
@@ -50,7 +50,8 @@ class nice_number(ctypes.Structure):
 class nice_niceonly_opts(ctypes.Structure):
     _fields_ = [("msd_floor", ctypes.c_uint64), ("chunk_size", ctypes.c_uint64),
                 ("threads", ctypes.c_int32), ("stride_k", ctypes.c_uint32),
-                ("msd_where", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
+                ("msd_where", ctypes.c_int32), ("deal_stride", ctypes.c_uint32),
+                ("deal_offset", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class nice_niceonly_stats(ctypes.Structure):
@@ -116,6 +117,7 @@ def lib():
         "nice_check_is_nice_inrange": ([u32, u64, u64], i32),
         "nice_check_msd_skippable_inrange": ([u32, u64, u64, u64, u64], i32),
         "nice_fd_segment_cuts": ([u32, P64, sz, PSZ], i32),
+        "nice_validate_detailed": ([u32, u64, u64, P64, PN, sz], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

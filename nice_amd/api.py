@@ -185,9 +185,14 @@ class GpuContext:
     # -- niceonly -------------------------------------------------------------
     def niceonly_raw(self, start: int, end: int, base: int, msd_floor: int = 0,
                      chunk_size: int = 0, threads: int = 0, stride_k: int = 0,
-                     msd_where: str = "auto", cap: int = 0):
+                     msd_where: str = "auto", cap: int = 0, deal_stride: int = 0,
+                     deal_offset: int = 0):
+        """Nice numbers of [start, end) ascending, and NiceonlyStats.  With
+        deal_stride N > 1 only the field's chunks c with c % N == deal_offset
+        are processed (rank deal_offset of an N-way job, nice_amd/dist.py)."""
         where = {"auto": 0, "host": 1, "device": 2}[msd_where]
-        opts = _lib.nice_niceonly_opts(msd_floor, chunk_size, threads, stride_k, where, 0)
+        opts = _lib.nice_niceonly_opts(msd_floor, chunk_size, threads, stride_k, where,
+                                       deal_stride, deal_offset, 0)
         st = _lib.nice_niceonly_stats()
         cap = max(cap, self._out_cap, 1024)
         while True:

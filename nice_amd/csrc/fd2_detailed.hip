@@ -60,6 +60,19 @@ constexpr bool split_exact(unsigned base, unsigned es, unsigned long long m) {
     return true;
 }
 
+// Tuning / bottleneck-probe knobs read from the environment exist only in
+// the probe build (make -C nice_amd probe -> libnice_hip_probe.so, used by
+// scripts/); the product library ignores the environment and always runs the
+// production configuration.
+#ifdef NICE_PROBES
+static u64 probe_knob(const char *name, u64 dflt) {
+    const char *v = getenv(name);
+    return v && *v ? strtoull(v, nullptr, 10) : dflt;
+}
+#else
+static constexpr u64 probe_knob(const char *, u64 dflt) { return dflt; }
+#endif
+
 template <int BASE_, int ND_, int NE_, int NE2_, int PROBE_ = 0, int WG_ = 512, int VD_ = 0>
 struct Cfg {
     static constexpr int BASE = BASE_;
@@ -701,8 +714,7 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
     // CU.  b40 1e9: 2.49 ms persistent at chunk 637, 2.31 persistent at ~80,
     // 2.19-2.21 at 60-120 non-persistent (scripts/gridx_probe.sh,
     // profiles/r01/fd2_chunk_sweep.log).
-    static const u64 tchunk_env = getenv("NICE_FD2_TCHUNK") ? strtoull(getenv("NICE_FD2_TCHUNK"), 0, 10) : 0;
-    const u64 tchunk = tchunk_env ? tchunk_env : (u64)P::TCHUNK;
+    const u64 tchunk = probe_knob("NICE_FD2_TCHUNK", (u64)P::TCHUNK);
     const uint4 *tabs = nullptr;
     if ((e = fd2_tables<P>(s, &tabs)) != hipSuccess) return e;
     DetailedLaunch q = p;
@@ -712,7 +724,7 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         // Chunk floor for fields too small to fill the chip: a lane's init
         // costs about ten steps, but with idle CUs latency wins (b40 1e6:
         // kernel 25 us at a floor of 32, 14 us at 4; scripts/small_fields.py).
-        const u64 min_chunk = getenv("NICE_FD2_MINCHUNK") ? strtoull(getenv("NICE_FD2_MINCHUNK"), 0, 10) : 4;
+        const u64 min_chunk = probe_knob("NICE_FD2_MINCHUNK", 4);
         // Whole rounds of workgroups, chunks <= the target (and <= B, the
         // low-digit table's reach).
         u64 rounds = (cnt + tchunk * lanes - 1) / (tchunk * lanes);
@@ -853,7 +865,8 @@ static const BaseThresholds &thresholds(uint32_t base) {
 // c: the limb counts of the segment's cut interval (cached in thresholds(),
 // no bignum work per launch).
 static hipError_t launch_segment(const DetailedLaunch &p, const Combo &c, int num_cus, hipStream_t s) {
-    const int probe = getenv("NICE_FD2_PROBE") ? atoi(getenv("NICE_FD2_PROBE")) : 0;
+    const int probe = (int)probe_knob("NICE_FD2_PROBE", 0);
+#ifdef NICE_PROBES
     if (probe && p.base == 40 && c.nd == 4 && c.ne == 8 && c.ne2 == 5) {
         if (probe == 1) return launch_cfg<Cfg<40, 4, 8, 5, 1>>(p, num_cus, s);
         if (probe == 2) return launch_cfg<Cfg<40, 4, 8, 5, 2>>(p, num_cus, s);
@@ -868,10 +881,11 @@ static hipError_t launch_segment(const DetailedLaunch &p, const Combo &c, int nu
         if (probe == 8) return launch_cfg<Cfg<40, 4, 8, 5, 0, 512, 1>>(p, num_cus, s);
         if (probe == 9) return launch_cfg<Cfg<40, 4, 8, 5, 0, 512, 2>>(p, num_cus, s);
     }
+#endif
     // Fields too small to fill the chip keep 512-thread workgroups (the
     // per-workgroup table build dominates there: b80 1e6 kernel 30 vs 38 us);
     // probe 20 forces them for b80 comparisons.
-    static const bool force512 = getenv("NICE_FD2_WG512") != nullptr;
+    const bool force512 = probe_knob("NICE_FD2_WG512", 0) != 0;
     const bool wg512 = force512 || p.count < 10000000ull || (probe == 20 && p.base == 80);
 #define X(B_, ND_, NE_, NE2_)                                                          \
     if (p.base == B_ && c.nd == ND_ && c.ne == NE_ && c.ne2 == NE2_)                    \

@@ -76,14 +76,22 @@ struct MsdNode {
     uint32_t depth, pad;
 };
 struct MsdLaunch {
-    uint64_t start_lo, start_hi;  // batch start (first chunk)
-    uint64_t batch_size;          // numbers in this batch (<= 2^63)
+    // The batch's level-0 nodes are the field's chunks c_j = deal_offset +
+    // (first + j) * deal_stride, j < nchunks: [start + c_j chunk, min(end,
+    // start + (c_j + 1) chunk)).  deal_stride 1 / offset 0 is a contiguous run
+    // of chunks; a rank of an N-way niceonly job is dealt every N-th chunk.
+    uint64_t start_lo, start_hi;  // field start (chunk grid origin)
+    uint64_t end_lo, end_hi;      // field end
+    uint64_t first;               // first dealt chunk of this batch (index among this caller's chunks)
+    uint64_t nchunks;             // chunks in this batch
+    uint64_t deal_stride, deal_offset;
     uint64_t chunk;               // MSD chunk size (client rule)
     uint64_t floor_size;          // recursion floor (250)
     MsdNode *q[2];                // ping-pong level queues
-    uint32_t *counters;           // [0..23] level sizes, [24] leaves (batch), [25] overflow
-                                  // flag, [26] leaves (sticky), [28..29] u64 candidates,
-                                  // [30..31] u64 numbers inside leaves (sticky)
+    uint32_t *counters;           // [0..23] level sizes, [24] leaf records (batch), [25]
+                                  // overflow flag, [26] MSD-surviving ranges (sticky),
+                                  // [28..29] u64 candidates, [30..31] u64 numbers inside
+                                  // the ranges (sticky)
     uint32_t q_cap;
     Leaf *leaves;
     uint32_t leaf_cap;
@@ -92,8 +100,11 @@ struct MsdLaunch {
     uint32_t R, M;
     uint32_t base;
     uint32_t in_range;            // the batch lies inside the base's valid range
-    uint32_t probe;               // timing experiments (NICE_MSD_PROBE): 1 no skip test, 2 no leaf stride math
+    uint32_t probe;               // probe build only (NICE_MSD_PROBE): 1 no skip test, 2 no leaf stride math
 };
+// A leaf's candidate count is capped at kLeafPiece: longer runs are stored as
+// several leaves, so niceonly_kernel's per-wave sums of 8 leaves fit 32 bits.
+constexpr uint32_t kLeafPiece = 1u << 28;
 // Enqueue the init + 22 level kernels (no host sync).
 hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s);
 

@@ -242,11 +242,47 @@ int emit_list(std::vector<Entry> &all, nice_number *out, size_t cap, size_t *n_o
     return NICE_OK;
 }
 
+// The server's submit invariants for a detailed result (api/src/main.rs:
+// 309-359): the distribution sums to the field size; for every bin above the
+// near-miss cutoff the count equals the number of listed numbers with that
+// unique count; the list holds exactly the numbers above the cutoff.  (The
+// server's last check, recomputing each listed number, runs on the device in
+// nice_process_range_detailed.)  get(i) -> {n, u} of list entry i.
+template <class Get>
+int validate_detailed(uint32_t base, u128 size, const uint64_t *hist, size_t n, Get get) {
+    u128 sum = 0;
+    for (uint32_t b = 0; b <= base; b++) sum += hist[b];
+    if (sum != size)
+        return fail(NICE_ERR_HIP, "self-check: distribution total does not equal the field size");
+    const uint32_t cutoff = nice::near_miss_cutoff(base);
+    std::vector<uint64_t> per(base + 1, 0);
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t u = get(i).u;
+        if (u <= cutoff || u > base)
+            return fail(NICE_ERR_HIP, "self-check: listed number " + std::to_string(i) +
+                                          " has num_uniques " + std::to_string(u) +
+                                          " at or below the cutoff");
+        per[u]++;
+    }
+    u128 above = 0;
+    for (uint32_t u = cutoff + 1; u <= base; u++) {
+        if (per[u] != hist[u])
+            return fail(NICE_ERR_HIP, "self-check: " + std::to_string(per[u]) +
+                                          " listed numbers with " + std::to_string(u) +
+                                          " uniques, distribution claims " + std::to_string(hist[u]));
+        above += hist[u];
+    }
+    if (above != (u128)n) return fail(NICE_ERR_HIP, "self-check: list length does not match the distribution");
+    return NICE_OK;
+}
+
+#ifdef NICE_PROBES
 // FD kernel variant (0 = production choice; others for scripts/fd_sweep.py).
 int fd_variant() {
     const char *v = getenv("NICE_FD_VARIANT");
     return v ? atoi(v) : 0;
 }
+#endif
 
 // Enqueue the detailed kernels for [s, e) on one device (async).
 int enqueue_detailed(Device &d, u128 s, u128 e, uint32_t base, bool &used_fd, uint64_t &fd_count) {
@@ -263,11 +299,16 @@ int enqueue_detailed(Device &d, u128 s, u128 e, uint32_t base, bool &used_fd, ui
             p.start_lo = lo64(a);
             p.start_hi = hi64(a);
             p.count = c;
+#ifdef NICE_PROBES
             const int var = fd_variant();
             hipError_t err = !fd ? nice::launch_detailed_generic(p, d.num_cus, d.stream)
                              : var == 0 && nice::fd2_supported(base)
                                  ? nice::launch_detailed_fd2(p, d.num_cus, d.stream)
                                  : nice::launch_detailed_fd(p, d.num_cus, d.stream, var);
+#else
+            hipError_t err = fd ? nice::launch_detailed_fd2(p, d.num_cus, d.stream)
+                                : nice::launch_detailed_generic(p, d.num_cus, d.stream);
+#endif
             if (err != hipSuccess)
                 return fail(NICE_ERR_HIP, std::string("detailed launch: ") + hipGetErrorString(err));
             if (fd) {
@@ -280,7 +321,12 @@ int enqueue_detailed(Device &d, u128 s, u128 e, uint32_t base, bool &used_fd, ui
         return NICE_OK;
     };
     u128 rs = 0, re = 0;
-    const bool fd = nice::fd_supported(base) && nice::base_range_cached(base, rs, re) == 1;
+#ifdef NICE_PROBES
+    const bool fd_base = nice::fd2_supported(base) || (fd_variant() && nice::fd_supported(base));
+#else
+    const bool fd_base = nice::fd2_supported(base);
+#endif
+    const bool fd = fd_base && nice::base_range_cached(base, rs, re) == 1;
     if (!fd) return launch(s, e, false);
     int rc;
     if ((rc = launch(s, std::min(e, rs), false))) return rc;
@@ -347,7 +393,7 @@ uint32_t nice_near_miss_cutoff(uint32_t base) { return nice::near_miss_cutoff(ba
 uint64_t nice_gpu_batch_size(void) { return 50000000ull; }
 uint64_t nice_processing_chunk_size(void) { return 1000000ull; }
 int nice_gpu_supports_base(uint32_t base) { return base >= 2 && base <= 128; }
-int nice_fd_kernel_base(uint32_t base) { return nice::fd_supported(base) ? 1 : 0; }
+int nice_fd_kernel_base(uint32_t base) { return nice::fd2_supported(base) ? 1 : 0; }
 
 int nice_last_kernel_stats(nice_ctx *ctx, int i, nice_kernel_stats *out) {
     if (!ctx || i < 0 || i >= (int)ctx->devs.size() || !out) return fail(NICE_ERR_INVALID, "bad args");
@@ -428,12 +474,48 @@ int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start
         }
     }
     std::memcpy(hist, total.data(), (base + 1) * 8);
-    // Self-check (the server's submit invariants, api/src/main.rs:309-359):
-    // counts sum to the field size and every near-miss bin matches the list.
-    u128 sum = 0;
-    for (uint32_t b = 0; b <= base; b++) sum += total[b];
-    if (sum != size) return fail(NICE_ERR_HIP, "histogram does not sum to the field size");
+    // Self-check: the server's submit invariants (api/src/main.rs:309-359)
+    // before anything is returned.
+    int rc = validate_detailed(base, size, total.data(), all.size(), [&](size_t i) { return all[i]; });
+    if (rc) return rc;
+    if (!all.empty()) {
+        // ... and its last one: every listed number's unique count recomputed
+        // by the generic per-n device function (full square / cube + digit
+        // scan, a different code path from the FD kernel that listed it).
+        Device &d = ctx->devs[0];
+        HIPCHK(hipSetDevice(d.id));
+        const size_t n = all.size();
+        std::vector<uint64_t> pairs(2 * n);
+        for (size_t i = 0; i < n; i++) {
+            pairs[2 * i] = lo64(all[i].n);
+            pairs[2 * i + 1] = hi64(all[i].n);
+        }
+        uint64_t *dn = nullptr;
+        uint32_t *du = nullptr;
+        HIPCHK(hipMalloc(&dn, n * 16));
+        HIPCHK(hipMalloc(&du, n * 4));
+        std::vector<uint32_t> u(n);
+        hipError_t err = hipMemcpyAsync(dn, pairs.data(), n * 16, hipMemcpyHostToDevice, d.stream);
+        if (err == hipSuccess) err = nice::launch_unique_counts(dn, (uint32_t)n, base, du, d.stream);
+        if (err == hipSuccess) err = hipMemcpyAsync(u.data(), du, n * 4, hipMemcpyDeviceToHost, d.stream);
+        if (err == hipSuccess) err = hipStreamSynchronize(d.stream);
+        (void)hipFree(dn);
+        (void)hipFree(du);
+        if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("self-check: ") + hipGetErrorString(err));
+        for (size_t i = 0; i < n; i++)
+            if (u[i] != all[i].u)
+                return fail(NICE_ERR_HIP, "self-check: unique count of a listed number does not recompute");
+    }
     return emit_list(all, out, cap, n_out);
+}
+
+int nice_validate_detailed(uint32_t base, uint64_t size_lo, uint64_t size_hi, const uint64_t *hist,
+                           const nice_number *list, size_t n) {
+    if (base < 2 || base > 128 || !hist || (n && !list)) return fail(NICE_ERR_INVALID, "bad args");
+    const int rc = validate_detailed(base, mk(size_lo, size_hi), hist, n, [&](size_t i) {
+        return Entry{mk(list[i].number_lo, list[i].number_hi), list[i].num_uniques};
+    });
+    return rc ? NICE_ERR_INVALID : NICE_OK;
 }
 
 int nice_debug_unique_counts(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t count,
@@ -545,8 +627,28 @@ int nice_stride_table(uint32_t base, uint32_t k, uint64_t *modulus, uint32_t *re
 }
 
 // ---------------------------------------------------------------------------
-// Niceonly: multi-threaded host MSD producer -> descriptor batches -> GPU.
+// Niceonly: device MSD (level kernels) or a multi-threaded host MSD producer
+// -> stride-index leaves -> the candidate kernel.
 // ---------------------------------------------------------------------------
+
+// NICE_GPU_MSD_FLOOR pins the reference GPU path's MSD floor
+// (client_process_gpu.rs:161-172: parsed as f64, used when >= 1, otherwise
+// ignored with a warning).  Read once, like the reference's OnceLock.
+static uint64_t env_msd_floor() {
+    static const uint64_t v = [] {
+        const char *e = getenv("NICE_GPU_MSD_FLOOR");
+        if (!e) return (uint64_t)0;
+        char *end = nullptr;
+        const double f = strtod(e, &end);
+        if (end == e || *end != 0 || !(f >= 1.0) || f > 1e18) {
+            fprintf(stderr, "nice: ignoring invalid NICE_GPU_MSD_FLOOR '%s'\n", e);
+            return (uint64_t)0;
+        }
+        return (uint64_t)f;
+    }();
+    return v;
+}
+
 int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi,
                                    uint64_t end_lo, uint64_t end_hi, uint32_t base,
                                    const nice_niceonly_opts *opts, nice_number *out, size_t cap,
@@ -559,14 +661,28 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
     if (s >= e)
         return fail(NICE_ERR_INVALID, "Range has invalid bounds, range_start must be < range_end");
     nice_niceonly_stats st{};
-    const uint64_t floor_size = opts && opts->msd_floor ? opts->msd_floor : 250;
+    uint64_t floor_size = opts && opts->msd_floor ? opts->msd_floor : env_msd_floor();
+    if (!floor_size) floor_size = 250;
     const uint32_t k = opts && opts->stride_k ? opts->stride_k : 2;
     int threads = opts && opts->threads > 0 ? opts->threads : (int)std::thread::hardware_concurrency();
     if (threads < 1) threads = 1;
     const u128 chunk = opts && opts->chunk_size ? (u128)opts->chunk_size : nice::client_chunk_size(e - s);
+    const uint64_t deal_stride = opts && opts->deal_stride ? opts->deal_stride : 1;
+    const uint64_t deal_offset = opts ? opts->deal_offset : 0;
+    if (deal_offset >= deal_stride) return fail(NICE_ERR_INVALID, "deal_offset must be < deal_stride");
+    // This caller's chunks of the field's grid: c = deal_offset + i * deal_stride.
+    const u128 nchunks_field = (e - s + chunk - 1) / chunk;
+    const u128 mine128 = deal_offset < nchunks_field
+                             ? (nchunks_field - deal_offset + deal_stride - 1) / deal_stride : 0;
+    if (mine128 >> 63) return fail(NICE_ERR_INVALID, "too many MSD chunks");
+    const uint64_t mine = (uint64_t)mine128;
+    auto chunk_range = [&](uint64_t i, u128 &cs, u128 &ce) {
+        cs = s + (u128)(deal_offset + (u128)i * deal_stride) * chunk;
+        ce = std::min(e, cs + chunk);
+    };
 
     std::lock_guard<std::mutex> lock(ctx->mu);
-    if (nice::residue_filter(base).empty()) {  // client_process_gpu.rs:525-531
+    if (nice::residue_filter(base).empty() || mine == 0) {  // client_process_gpu.rs:525-531
         if (stats) *stats = st;
         if (n_out) *n_out = 0;
         return NICE_OK;
@@ -603,39 +719,44 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
         if (rc) return rc;
     }
 
-    // Device MSD: batches of whole client chunks, each run as init + 23
+    // Device MSD: batches of this caller's chunks, each run as init + the
     // level kernels + the candidate kernel, all stream-ordered (no host sync
     // until the end).  Batches alternate over the context's devices.
     auto run_device = [&]() -> int {
         if (chunk > ((u128)1 << 40)) return fail(NICE_ERR_INVALID, "device MSD: chunk_size too large");
+        if ((e - s) >> 63) return fail(NICE_ERR_INVALID, "device MSD: field larger than 2^63");
         const uint64_t cnk = (uint64_t)chunk;
-        const uint64_t nchunks = (uint64_t)((e - s + chunk - 1) / chunk);
         // Nodes per level and leaves per batch are <= batch / floor + chunks
         // (every split child holds >= floor numbers); size batches for 2^24.
         const uint64_t fl = std::min<uint64_t>(floor_size, 1ull << 30);
         uint64_t cpb = std::max<uint64_t>(1, (fl << 24) / cnk);
-        cpb = std::min(cpb, nchunks);
+        cpb = std::min(cpb, mine);
         const uint64_t batch_n = cpb * cnk;
         uint64_t per = std::min<uint64_t>(batch_n / fl + cpb, cpb << 22) + 64;
         per = std::min<uint64_t>(per, 1ull << 26);
+        // leaf records: one per range plus one per kLeafPiece candidates
+        const uint64_t leaf_cap = std::min<uint64_t>(per + (batch_n / nice::kLeafPiece) + 64, 0xffffffffull);
         for (auto &d : ctx->devs) {
             HIPCHK(hipSetDevice(d.id));
-            int r = ensure_msd(d, (uint32_t)per, (uint32_t)per);
+            int r = ensure_msd(d, (uint32_t)per, (uint32_t)leaf_cap);
             if (r) return r;
             HIPCHK(hipMemsetAsync(d.msd.counters, 0, 32 * 4, d.stream));
         }
-        const uint64_t nbatches = (nchunks + cpb - 1) / cpb;
+        const uint64_t nbatches = (mine + cpb - 1) / cpb;
         for (uint64_t bi = 0; bi < nbatches; bi++) {
             Device &d = ctx->devs[bi % ctx->devs.size()];
             HIPCHK(hipSetDevice(d.id));
-            const u128 bs = s + (u128)bi * batch_n;
-            const uint64_t bsize = (uint64_t)std::min<u128>(batch_n, e - bs);
             if (bi >= ctx->devs.size())  // first batch per device: zeroed above
                 HIPCHK(hipMemsetAsync(d.msd.counters, 0, 25 * 4, d.stream));
             nice::MsdLaunch mp{};
-            mp.start_lo = lo64(bs);
-            mp.start_hi = hi64(bs);
-            mp.batch_size = bsize;
+            mp.start_lo = lo64(s);
+            mp.start_hi = hi64(s);
+            mp.end_lo = lo64(e);
+            mp.end_hi = hi64(e);
+            mp.first = bi * cpb;
+            mp.nchunks = std::min(cpb, mine - bi * cpb);
+            mp.deal_stride = deal_stride;
+            mp.deal_offset = deal_offset;
             mp.chunk = cnk;
             mp.floor_size = floor_size;
             mp.q[0] = d.msd.q[0];
@@ -650,7 +771,9 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
             mp.M = (uint32_t)M;
             mp.base = base;
             mp.in_range = in_range;
+#ifdef NICE_PROBES
             mp.probe = getenv("NICE_MSD_PROBE") ? (uint32_t)atoi(getenv("NICE_MSD_PROBE")) : 0u;
+#endif
             hipError_t err = nice::launch_msd_device(mp, d.num_cus, d.stream);
             if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("msd launch: ") + hipGetErrorString(err));
             nice::NiceonlyLaunch p{};
@@ -673,11 +796,13 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
                                   d.stream));
             HIPCHK(hipStreamSynchronize(d.stream));
             const uint32_t *c = d.msd.h_counters;
+#ifdef NICE_PROBES
             if (getenv("NICE_MSD_TRACE")) {  // level sizes of the last batch (diagnostics)
                 fprintf(stderr, "msd levels:");
                 for (int lv = 0; lv < 24; lv++) fprintf(stderr, " %u", c[lv]);
-                fprintf(stderr, " | leaves %u\n", c[26]);
+                fprintf(stderr, " | ranges %u\n", c[26]);
             }
+#endif
             if (c[25])
                 return fail(NICE_ERR_CAPACITY, "device MSD queue overflow (msd_floor too small for "
                                                "chunk_size); use msd_where = host");
@@ -693,19 +818,19 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
 
     const int where = opts ? opts->msd_where : NICE_MSD_AUTO;
     if (where < NICE_MSD_AUTO || where > NICE_MSD_DEVICE) return fail(NICE_ERR_INVALID, "bad msd_where");
-    const bool on_device = where == NICE_MSD_DEVICE || (where == NICE_MSD_AUTO && k == 2);
+    const bool on_device = where == NICE_MSD_DEVICE ||
+                           (where == NICE_MSD_AUTO && k == 2 && !((e - s) >> 63) && chunk <= ((u128)1 << 40));
     int rc = NICE_OK;
     if (on_device) {
         rc = run_device();
     } else {
         // Producer: worker threads run the MSD filter per chunk and hand the
         // surviving ranges to this thread in chunk batches.
-        const uint64_t nchunks = (uint64_t)((e - s + chunk - 1) / chunk);
         std::atomic<uint64_t> next{0};
         std::mutex qmu;
         std::condition_variable qcv;
         std::deque<std::vector<std::pair<u128, u128>>> queue;
-        const int n_workers = (int)std::min<uint64_t>(threads, nchunks);
+        const int n_workers = (int)std::min<uint64_t>(threads, mine);
         int live = n_workers;  // guarded by qmu
         std::vector<std::thread> workers;
         std::unique_ptr<nice::MsdRunner> filt = nice::make_msd(base);
@@ -714,9 +839,9 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
                 std::vector<std::pair<u128, u128>> local;
                 for (;;) {
                     uint64_t i = next.fetch_add(1);
-                    if (i >= nchunks) break;
-                    u128 cs = s + (u128)i * chunk;
-                    u128 ce = std::min(e, cs + chunk);
+                    if (i >= mine) break;
+                    u128 cs, ce;
+                    chunk_range(i, cs, ce);
                     filt->ranges(cs, ce, floor_size, local);
                     if (local.size() >= 4096) {
                         std::lock_guard<std::mutex> g(qmu);
@@ -741,9 +866,9 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
             HIPCHK(hipSetDevice(d.id));
             LeafBuf &b = d.desc[d.desc_next];
             d.desc_next ^= 1;
-            // One leaf per range, more for ranges holding over 2^30 candidates
-            // (the kernel's residue-sequence index is 32-bit).
-            constexpr u128 kPiece = (u128)1 << 30;
+            // One leaf per range, more for ranges holding over kLeafPiece
+            // candidates (the kernel sums 8 leaves' counts in 32 bits).
+            constexpr u128 kPiece = nice::kLeafPiece;
             size_t need = 0;
             for (auto &pr : pend) {
                 const u128 c = table->index_of(pr.second) - table->index_of(pr.first);

@@ -271,16 +271,22 @@ __device__ __forceinline__ u32 wave_reserve(u32 *ctr, u32 mine) {
     return __shfl(base, 0) + incl - mine;
 }
 
+// Level 0: this batch's chunks of the field (dealt: every deal_stride-th
+// chunk from deal_offset), each clipped to the field's end.
 __global__ void msd_init_kernel(MsdLaunch p) {
-    const u64 nchunks = (p.batch_size + p.chunk - 1) / p.chunk;
-    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nchunks;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < p.nchunks;
          i += (u64)gridDim.x * blockDim.x) {
+        const u64 c = p.deal_offset + (p.first + i) * p.deal_stride;
         u64 lo = p.start_lo, hi = p.start_hi;
-        add_u128(lo, hi, i * p.chunk);
-        const u64 size = (p.batch_size - i * p.chunk) < p.chunk ? (p.batch_size - i * p.chunk) : p.chunk;
+        // c * chunk < field size < 2^64 (checked by the host)
+        add_u128(lo, hi, c * p.chunk);
+        // numbers left in the field from this chunk's start: end - lo (u128)
+        const u64 rem_lo = p.end_lo - lo;
+        const u64 rem_hi = p.end_hi - hi - (p.end_lo < lo ? 1 : 0);
+        const u64 size = rem_hi || rem_lo > p.chunk ? p.chunk : rem_lo;
         p.q[0][i] = MsdNode{lo, hi, size, 0u, 0u};
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) p.counters[0] = (u32)nchunks;
+    if (blockIdx.x == 0 && threadIdx.x == 0) p.counters[0] = (u32)p.nchunks;
 }
 
 // Reserve `mine` slots per thread of a 256-thread workgroup with ONE atomic
@@ -337,7 +343,12 @@ msd_level_kernel(MsdLaunch p, u32 level, G g) {
             if (!leaf) {
                 u64 l_lo = nd.lo, l_hi = nd.hi;
                 add_u128(l_lo, l_hi, nd.size - 1);
-                if (nd.size != 1 && !(p.probe & 1)) {
+#ifdef NICE_PROBES
+                const bool no_skip_test = p.probe & 1;
+#else
+                constexpr bool no_skip_test = false;
+#endif
+                if (nd.size != 1 && !no_skip_test) {
                     if constexpr (IsConst<G>::value) {
                         skip = p.in_range ? msd_skippable_fast<IsConst<G>::base>(nd.lo, nd.hi, l_lo, l_hi)
                                           : msd_skippable<G>(nd.lo, nd.hi, l_lo, l_hi, g);
@@ -350,24 +361,37 @@ msd_level_kernel(MsdLaunch p, u32 level, G g) {
             act = skip ? 0u : (leaf ? 1u : 2u);
         }
         LeafDesc ld{0, 0, 0, 0};
+#ifdef NICE_PROBES
         if (act == 1 && (p.probe & 2)) {
             ld = LeafDesc{nd.lo, nd.hi, nd.size, 0};
-        } else if (act == 1) {
-            ld = leaf_desc<MC>(nd.lo, nd.hi, nd.size, p);
-            if (ld.count == 0) act = 0;
-        }
-        // leaves
-        const u32 pos = block_reserve(&p.counters[24], act == 1 ? 1u : 0u, slots);
-        bool stored = false;
+        } else
+#endif
         if (act == 1) {
-            if (pos >= p.leaf_cap || ld.count > 0xffffffffull) {
+            ld = leaf_desc<MC>(nd.lo, nd.hi, nd.size, p);
+        }
+        // Leaf records: one per kLeafPiece candidates (a range without
+        // candidates still counts as an MSD-surviving range, none stored).
+        const u64 pieces64 = act == 1 ? (ld.count + kLeafPiece - 1) / kLeafPiece : 0;
+        const u32 pieces = pieces64 > 0xffffu ? 0xffffu : (u32)pieces64;
+        const u32 pos = block_reserve(&p.counters[24], pieces, slots);
+        if (act == 1) {
+            if (pieces64 > 0xffffu || (u64)pos + pieces > p.leaf_cap) {
                 atomicOr(&p.counters[25], 1u);
             } else {
-                p.leaves[pos] = Leaf{ld.b0_lo, ld.b0_hi, ld.g0, (u32)ld.count};
-                stored = true;
+                u64 b0_lo = ld.b0_lo, b0_hi = ld.b0_hi;
+                u64 g = ld.g0;  // residue-sequence index relative to b0
+                for (u32 q = 0; q < pieces; q++) {
+                    if (g >= p.R) {  // re-base: g < R keeps the kernel's index 32-bit
+                        const u64 cyc = g / p.R;
+                        add_u128(b0_lo, b0_hi, cyc * p.M);
+                        g -= cyc * p.R;
+                    }
+                    const u64 left = ld.count - (u64)q * kLeafPiece;
+                    const u32 cnt = left < kLeafPiece ? (u32)left : kLeafPiece;
+                    p.leaves[pos + q] = Leaf{b0_lo, b0_hi, (u32)g, cnt};
+                    g += cnt;
+                }
             }
-        }
-        if (stored) {
             n_st++;
             c_st += ld.count;
             s_st += nd.size;
@@ -441,7 +465,7 @@ hipError_t launch_niceonly(const NiceonlyLaunch &p, int num_cus, hipStream_t s) 
 template <class G, u32 MC = 0>
 static hipError_t launch_msd(const MsdLaunch &p, const G &g, int num_cus, hipStream_t s) {
     hipLaunchKernelGGL(msd_init_kernel, dim3(256), dim3(256), 0, s, p);
-    const u64 nchunks = (p.batch_size + p.chunk - 1) / p.chunk;
+    const u64 nchunks = p.nchunks;
     // A node of level d has at most ceil(chunk / 2^d) numbers and splits only
     // if it holds >= 2 * floor, so levels past the first d with
     // ceil(chunk / 2^d) < 2 * floor are empty: launch only levels 0..last

@@ -13,12 +13,19 @@ non-empty (near-misses and nice numbers are rare: usually no second
 collective).  `process_field_both_dist` does detailed and niceonly of a field
 with that single all-reduce.
 
-Shards are contiguous and ordered by rank, so concatenating the gathered lists
-in rank order is already ascending (the reference sorts after the fact,
-client_process_gpu.rs:792, 873).  Niceonly shards are cut on the client chunk
-grid of the WHOLE field (client/src/main.rs:158-168) and each rank is told
-that chunk size, so the MSD recursion sees exactly the chunks the single-
-process CPU path would, and the candidate set is unchanged by sharding.
+Detailed shards are contiguous and ordered by rank, so concatenating the
+gathered near-miss lists in rank order is already ascending.  Niceonly work is
+DEALT, not sliced: the whole field is cut on its client chunk grid
+(client/src/main.rs:158-168) and rank r processes chunks c with c % N == r.
+MSD survival is very uneven along a field (the b50 massive field's first 70 %
+is pruned entirely), so contiguous slabs would leave most ranks idle; dealt
+chunks give every rank a sample of the whole field, the way the reference
+feeds descriptors from a shared channel (client_process_gpu.rs:589-709).  Each
+chunk's MSD recursion is exactly the single-process CPU path's, so the
+candidate set is unchanged; the gathered nice list is sorted (the reference
+sorts after the fact too, client_process_gpu.rs:792).  A rank whose detailed
+shard is empty (a field smaller than the world) contributes zeros to the
+collective instead of calling the library.
 
 With the nccl backend the collectives are RCCL over xGMI on device tensors;
 with gloo (the CPU tests) they run on host tensors.  `shard_fn` lets tests
@@ -49,6 +56,17 @@ def shard_bounds(start: int, end: int, rank: int, world: int, grain: int = 1) ->
     u0 = rank * per + min(rank, extra)
     u1 = u0 + per + (1 if rank < extra else 0)
     return min(end, start + u0 * grain), min(end, start + u1 * grain)
+
+
+def dealt_chunks(start: int, end: int, chunk: int, stride: int, offset: int):
+    """The chunks [c_s, c_e) of [start, end)'s chunk grid with index c %
+    stride == offset, ascending (what nice_process_range_niceonly_ex processes
+    with deal_stride / deal_offset)."""
+    c = offset
+    while start + c * chunk < end:
+        a = start + c * chunk
+        yield a, min(end, a + chunk)
+        c += stride
 
 
 def _device(dist, group):
@@ -117,7 +135,7 @@ def process_range_detailed_dist(range_: FieldSize, base: int, ctx=None, group=No
     s, e = shard_bounds(range_.range_start, range_.range_end, rank, world)
     if shard_fn is None:
         shard_fn = ctx.detailed_raw
-    hist, lst = shard_fn(s, e, base)
+    hist, lst = shard_fn(s, e, base) if s < e else ([0] * (base + 1), [])
     red = _all_reduce_ints(list(hist[: base + 1]) + _onehot(rank, world, len(lst)), dist, group)
     hist, counts = red[: base + 1], red[base + 1:]
     rows = _gather_rows(lst, dist, group, counts=counts)
@@ -126,26 +144,37 @@ def process_range_detailed_dist(range_: FieldSize, base: int, ctx=None, group=No
         nice_numbers=[NiceNumberSimple(n, u) for n, u in rows])
 
 
-def niceonly_shard_bounds(range_: FieldSize, rank: int, world: int, chunk: int = 0):
-    """Rank r's niceonly shard: cut on the whole field's client chunk grid."""
+def niceonly_deal(range_: FieldSize, rank: int, world: int, chunk: int = 0):
+    """Rank r's niceonly work: the whole field's chunk grid, every world-th
+    chunk from r.  Returns the library options that select it, or None when
+    the field has fewer chunks than r + 1."""
     chunk = chunk or client_chunk_size(range_.range_size)
-    s, e = shard_bounds(range_.range_start, range_.range_end, rank, world, grain=chunk)
-    return s, e, chunk
+    if range_.range_start + rank * chunk >= range_.range_end:
+        return None
+    return {"chunk_size": chunk, "deal_stride": world, "deal_offset": rank}
+
+
+def _zeros(base: int):
+    return [0] * (base + 1)
 
 
 def _both_shards(range_: FieldSize, base: int, ctx, rank: int, world: int, nice_opts):
-    """This rank's detailed shard and niceonly shard of `range_`, through
+    """This rank's detailed shard and niceonly deal of `range_`, through
     ctx.both_raw when the context has it (GpuContext: in sequence; BothModes:
     at once, on two streams), else detailed_raw then niceonly_raw."""
     s, e = shard_bounds(range_.range_start, range_.range_end, rank, world)
-    ns, ne, chunk = niceonly_shard_bounds(range_, rank, world, nice_opts.pop("chunk_size", 0))
-    nice_range = (ns, ne) if ns < ne else None
+    det_range = (s, e) if s < e else None
+    nice_opts = dict(nice_opts)
+    deal = niceonly_deal(range_, rank, world, nice_opts.pop("chunk_size", 0))
+    nice_range = (range_.range_start, range_.range_end) if deal else None
+    if deal:
+        nice_opts.update(deal)
     if hasattr(ctx, "both_raw"):
-        return ctx.both_raw((s, e), nice_range, base, chunk_size=chunk, **nice_opts)
-    det = ctx.detailed_raw(s, e, base)
-    nice = ctx.niceonly_raw(ns, ne, base, chunk_size=chunk, **nice_opts) if nice_range \
-        else ([], None)
-    return det, nice
+        (hist, near), nice = ctx.both_raw(det_range, nice_range, base, **nice_opts)
+    else:
+        hist, near = ctx.detailed_raw(s, e, base) if det_range else (None, [])
+        nice = ctx.niceonly_raw(*nice_range, base, **nice_opts) if nice_range else ([], None)
+    return (hist if hist is not None else _zeros(base), near), nice
 
 
 def process_field_both_dist(range_: FieldSize, base: int, ctx, group=None,
@@ -162,8 +191,8 @@ def process_field_both_dist(range_: FieldSize, base: int, ctx, group=None,
                            + _onehot(rank, world, len(nice)), dist, group)
     hist = red[: base + 1]
     near_rows = _gather_rows(near, dist, group, counts=red[base + 1: base + 1 + world])
-    nice_rows = _gather_rows([(n, base) for n in nice], dist, group,
-                             counts=red[base + 1 + world:])
+    nice_rows = sorted(_gather_rows([(n, base) for n in nice], dist, group,
+                                    counts=red[base + 1 + world:]))
     det = FieldResults(
         distribution=[UniquesDistributionSimple(i, hist[i]) for i in range(1, base + 1)],
         nice_numbers=[NiceNumberSimple(n, u) for n, u in near_rows])
@@ -265,8 +294,8 @@ def finish_both(ex: PipelinedExchange, collected):
     world = ex.dist.get_world_size(ex.group)
     hist = red[: base + 1]
     near_rows = _gather_rows(near, ex.dist, ex.group, counts=red[base + 1: base + 1 + world])
-    nice_rows = _gather_rows([(n, base) for n in nice], ex.dist, ex.group,
-                             counts=red[base + 1 + world:])
+    nice_rows = sorted(_gather_rows([(n, base) for n in nice], ex.dist, ex.group,
+                                    counts=red[base + 1 + world:]))
     det = FieldResults(
         distribution=[UniquesDistributionSimple(i, hist[i]) for i in range(1, base + 1)],
         nice_numbers=[NiceNumberSimple(n, u) for n, u in near_rows])
@@ -276,17 +305,17 @@ def finish_both(ex: PipelinedExchange, collected):
 
 def process_range_niceonly_dist(range_: FieldSize, base: int, ctx=None, group=None,
                                 shard_fn: Optional[Callable] = None, **opts) -> FieldResults:
-    """process_range_niceonly over a process group (shards on the whole
-    field's client chunk grid, see module doc)."""
+    """process_range_niceonly over a process group: rank r is dealt every
+    world-th chunk of the field's chunk grid (see module doc).  shard_fn(start,
+    end, base, **deal) stands in for ctx.niceonly_raw in the CPU tests."""
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    s, e, chunk = niceonly_shard_bounds(range_, rank, world, opts.pop("chunk_size", 0))
-    if s < e:
+    deal = niceonly_deal(range_, rank, world, opts.pop("chunk_size", 0))
+    lst = []
+    if deal:
         if shard_fn is None:
-            lst, _ = ctx.niceonly_raw(s, e, base, chunk_size=chunk, **opts)
+            lst, _ = ctx.niceonly_raw(range_.range_start, range_.range_end, base, **deal, **opts)
         else:
-            lst = shard_fn(s, e, base, chunk)
-    else:
-        lst = []
-    rows = _gather_rows([(n, base) for n in lst], dist, group)
+            lst = shard_fn(range_.range_start, range_.range_end, base, **deal)
+    rows = sorted(_gather_rows([(n, base) for n in lst], dist, group))
     return FieldResults(distribution=[], nice_numbers=[NiceNumberSimple(n, u) for n, u in rows])

@@ -384,10 +384,11 @@ typedef struct {
     /* niceonly */
     u64 *stride_res; u64 stride_count; u64 stride_mod;
     u64 *cand_counts;
+    u64 *range_counts;
 } job;
 
 static uint64_t niceonly_range_impl(u128 s, u128 e, u32 base, const u64 *res, u64 R,
-                                    u64 M, u64 floor_size, misslist *out);
+                                    u64 M, u64 floor_size, misslist *out, u64 *n_ranges);
 
 static void *worker(void *arg) {
     job *j = (job *)arg;
@@ -401,7 +402,8 @@ static void *worker(void *arg) {
         } else {
             j->cand_counts[i] = niceonly_range_impl(s, e, j->base, j->stride_res,
                                                     j->stride_count, j->stride_mod,
-                                                    j->floor_size, &j->lists[i]);
+                                                    j->floor_size, &j->lists[i],
+                                                    &j->range_counts[i]);
         }
     }
     return NULL;
@@ -642,10 +644,12 @@ u64 oracle_valid_ranges(u64 slo, u64 shi, u64 elo, u64 ehi, u32 base, u64 floor_
 
 /* client_process.rs:439-465 + stride_filter.rs:139-155 */
 static uint64_t niceonly_range_impl(u128 s, u128 e, u32 base, const u64 *res, u64 R,
-                                    u64 M, u64 floor_size, misslist *out) {
+                                    u64 M, u64 floor_size, misslist *out, u64 *n_ranges) {
+    if (n_ranges) *n_ranges = 0;
     if (R == 0) return 0;
     rangelist rl = {0};
     valid_ranges_rec(s, e, base, 0, 22, floor_size, 2, &rl);
+    if (n_ranges) *n_ranges = rl.len;
     uint64_t cands = 0;
     for (u64 q = 0; q < rl.len; q++) {
         u64 idx;
@@ -682,36 +686,53 @@ u64 oracle_process_range_niceonly(u64 slo, u64 shi, u64 elo, u64 ehi, u32 base, 
     u64 R, M;
     u64 *res = stride_table_alloc(base, k, &R, &M);
     misslist ml = {0};
-    u64 c = niceonly_range_impl(mk(slo, shi), mk(elo, ehi), base, res, R, M, floor_size, &ml);
+    u64 c = niceonly_range_impl(mk(slo, shi), mk(elo, ehi), base, res, R, M, floor_size, &ml,
+                                NULL);
     if (n_candidates) *n_candidates = c;
     u64 n = emit_nice(&ml, out, cap);
     free(ml.n); free(ml.u); free(res);
     return n;
 }
 
-u64 oracle_process_field_niceonly_mt(u64 slo, u64 shi, u64 elo, u64 ehi, u32 base,
-                                     int threads, u64 *out, u64 cap, u64 *n_candidates) {
+/* client/src/main.rs:120-254 (niceonly) with an explicit MSD chunk size
+ * (0 -> the client rule) and floor (0 -> 250): a window of a larger field is
+ * processed on that field's chunk grid when it starts on a grid point.
+ * *n_ranges receives the number of MSD-surviving ranges (get_valid_ranges
+ * output length summed over chunks, msd_prefix_filter.rs:665-674). */
+u64 oracle_process_field_niceonly_ex(u64 slo, u64 shi, u64 elo, u64 ehi, u32 base,
+                                     int threads, u64 chunk, u64 floor_size, u64 *out,
+                                     u64 cap, u64 *n_candidates, u64 *n_ranges) {
     job j;
     memset(&j, 0, sizeof(j));
     j.start = mk(slo, shi); j.end = mk(elo, ehi); j.base = base; j.mode = 1;
-    j.floor_size = 250; /* MSD_RECURSIVE_MIN_RANGE_SIZE, msd_prefix_filter.rs:282 */
-    j.chunk = client_chunk_size(j.end - j.start);
+    j.floor_size = floor_size ? floor_size : 250; /* MSD_RECURSIVE_MIN_RANGE_SIZE, msd_prefix_filter.rs:282 */
+    j.chunk = chunk ? (u128)chunk : client_chunk_size(j.end - j.start);
     j.nchunks = (u64)((j.end - j.start + j.chunk - 1) / j.chunk);
     atomic_init(&j.next, 0);
     j.stride_res = stride_table_alloc(base, 2, &j.stride_count, &j.stride_mod);
     j.lists = calloc(j.nchunks, sizeof(misslist));
     j.cand_counts = calloc(j.nchunks, sizeof(u64));
+    j.range_counts = calloc(j.nchunks, sizeof(u64));
     run_job(&j, threads);
     misslist all = {0};
-    u64 cands = 0;
+    u64 cands = 0, ranges = 0;
     for (u64 i = 0; i < j.nchunks; i++) {
         for (size_t q = 0; q < j.lists[i].len; q++)
             ml_push(&all, mk(j.lists[i].n[2 * q], j.lists[i].n[2 * q + 1]), base);
         cands += j.cand_counts[i];
+        ranges += j.range_counts[i];
         free(j.lists[i].n); free(j.lists[i].u);
     }
     if (n_candidates) *n_candidates = cands;
+    if (n_ranges) *n_ranges = ranges;
     u64 n = emit_nice(&all, out, cap);
-    free(all.n); free(all.u); free(j.lists); free(j.cand_counts); free(j.stride_res);
+    free(all.n); free(all.u); free(j.lists); free(j.cand_counts); free(j.range_counts);
+    free(j.stride_res);
     return n;
+}
+
+u64 oracle_process_field_niceonly_mt(u64 slo, u64 shi, u64 elo, u64 ehi, u32 base,
+                                     int threads, u64 *out, u64 cap, u64 *n_candidates) {
+    return oracle_process_field_niceonly_ex(slo, shi, elo, ehi, base, threads, 0, 0, out, cap,
+                                            n_candidates, NULL);
 }

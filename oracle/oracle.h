@@ -111,6 +111,13 @@ uint64_t oracle_process_field_niceonly_mt(uint64_t start_lo, uint64_t start_hi,
                                           uint64_t end_lo, uint64_t end_hi, uint32_t base,
                                           int threads, uint64_t *out, uint64_t cap,
                                           uint64_t *n_candidates);
+/* The same with an explicit MSD chunk size (0 -> client rule) and floor (0 ->
+ * 250); *n_ranges receives the number of MSD-surviving ranges. */
+uint64_t oracle_process_field_niceonly_ex(uint64_t start_lo, uint64_t start_hi,
+                                          uint64_t end_lo, uint64_t end_hi, uint32_t base,
+                                          int threads, uint64_t chunk, uint64_t floor_size,
+                                          uint64_t *out, uint64_t cap, uint64_t *n_candidates,
+                                          uint64_t *n_ranges);
 
 #ifdef __cplusplus
 }

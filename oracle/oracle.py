@@ -67,6 +67,9 @@ def lib():
         L.oracle_process_field_niceonly_mt.argtypes = [u64, u64, u64, u64, u32, i32, P64, u64,
                                                        P64]
         L.oracle_process_field_niceonly_mt.restype = u64
+        L.oracle_process_field_niceonly_ex.argtypes = [u64, u64, u64, u64, u32, i32, u64, u64,
+                                                       P64, u64, P64, P64]
+        L.oracle_process_field_niceonly_ex.restype = u64
         _lib = L
     return _lib
 
@@ -196,3 +199,17 @@ def process_field_niceonly_mt(start: int, end: int, base: int, threads: int,
         raise OverflowError("nice list exceeded capacity")
     nice = [(buf[2 * i] | (buf[2 * i + 1] << 64), base) for i in range(n)]
     return FieldResults([], nice), cands.value
+
+
+def process_field_niceonly_ex(start: int, end: int, base: int, threads: int, chunk: int = 0,
+                              floor_size: int = 0, cap: int = 1 << 16):
+    """process_field_niceonly_mt with an explicit MSD chunk size (0 = client
+    rule) and floor (0 = 250).  Returns (FieldResults, candidates, ranges)."""
+    buf = (ctypes.c_uint64 * (2 * cap))()
+    cands, ranges = ctypes.c_uint64(), ctypes.c_uint64()
+    n = lib().oracle_process_field_niceonly_ex(*_split(start), *_split(end), base, threads, chunk,
+                                               floor_size, buf, cap, cands, ranges)
+    if n > cap:
+        raise OverflowError("nice list exceeded capacity")
+    nice = [(buf[2 * i] | (buf[2 * i + 1] << 64), base) for i in range(n)]
+    return FieldResults([], nice), cands.value, ranges.value

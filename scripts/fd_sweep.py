@@ -7,6 +7,8 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+import probe_lib  # noqa: E402,F401  (knobs exist only in the probe build)
 import nice_amd as N  # noqa: E402
 
 cfg = [(40, 10 ** 9), (50, 10 ** 9), (80, 2 * 10 ** 8)]

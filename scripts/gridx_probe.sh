@@ -7,7 +7,7 @@ cd /root/repo
 for cfg in "$@"; do
   set -- $cfg
   NICE_FD2_TCHUNK=$2 timeout -k 10 90 python -c "
-import sys, statistics; sys.path.insert(0, '.')
+import sys, statistics; sys.path.insert(0, '.'); sys.path.insert(0, 'scripts'); import probe_lib
 import nice_amd as N
 ctx = N.GpuContext(0); s = N.get_base_range_u128($1).range_start
 h, l = ctx.detailed_raw(s, s + 10**9, $1); ref = (list(h), sorted(l))

@@ -8,6 +8,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+import probe_lib  # noqa: E402,F401  (knobs exist only in the probe build)
 import nice_amd as N  # noqa: E402
 
 EXACT = {0, 5, 6, 7, 8, 9}

@@ -8,6 +8,9 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+if os.environ.get("NICE_PROBE_LIB"):  # probe build (NICE_MSD_PROBE etc., scripts/gpu_msdprobe.sh)
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import probe_lib  # noqa: E402,F401
 import nice_amd as N  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5

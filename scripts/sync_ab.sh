@@ -5,7 +5,7 @@
 set -e
 cd /root/repo
 for i in 1 2; do
-  NICE_FD2_WG512=1 timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/ab_wg512_$i.json
+  # (the workgroup-size leg needs the probe build: scripts/wg_ab.sh)
   timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/ab_default_$i.json
   timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 --sequential > gpurun_out/ab_seq_$i.json
 done

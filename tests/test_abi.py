@@ -207,3 +207,56 @@ def test_msd_fast_path_matches_oracle(base):
         hits += want
         assert L.nice_check_msd_skippable_inrange(base, *_split(a), *_split(b)) == want, (a, b)
     assert 0 < hits < len(cases)
+
+
+def _validate(base, size, hist, lst):
+    arr = (_lib.nice_number * max(len(lst), 1))()
+    for i, (n, u) in enumerate(lst):
+        arr[i].number_lo, arr[i].number_hi, arr[i].num_uniques = n & ((1 << 64) - 1), n >> 64, u
+    h = (ctypes.c_uint64 * (base + 1))(*hist)
+    return _lib.lib().nice_validate_detailed(base, size & ((1 << 64) - 1), size >> 64, h, arr,
+                                             len(lst))
+
+
+def test_self_check_rejects_corrupted_results():
+    """nice_validate_detailed = the server's submit checks (api/src/main.rs:
+    309-359), applied by nice_process_range_detailed to its own output: a
+    correct oracle result passes, every kind of corruption fails."""
+    s, e = 10 ** 6, 10 ** 6 + 10 ** 4
+    r = O.process_range_detailed(s, e, 10)
+    hist = [0] + [c for _, c in r.distribution]
+    lst = list(r.nice_numbers)
+    assert len(lst) == 5395
+    assert _validate(10, e - s, hist, lst) == _lib.NICE_OK
+    bad = hist[:]
+    bad[5] += 1  # mass no longer equals the field size
+    assert _validate(10, e - s, bad, lst) == _lib.NICE_ERR_INVALID
+    assert b"field size" in _lib.lib().nice_last_error()
+    bad = hist[:]
+    bad[10] -= 1
+    bad[9] += 1  # same mass, near-miss bin disagrees with the list
+    assert _validate(10, e - s, bad, lst) == _lib.NICE_ERR_INVALID
+    assert _validate(10, e - s, hist, lst[:-1]) == _lib.NICE_ERR_INVALID  # dropped entry
+    assert _validate(10, e - s, hist, lst + [lst[0]]) == _lib.NICE_ERR_INVALID  # duplicate
+    assert _validate(10, e - s, hist, lst[:-1] + [(lst[-1][0], 9)]) == _lib.NICE_ERR_INVALID
+    s40 = O.base_range(40)[0]
+    r = O.process_range_detailed(s40, s40 + 10 ** 4, 40)
+    assert _validate(40, 10 ** 4, [0] + [c for _, c in r.distribution], []) == _lib.NICE_OK
+
+
+def test_product_library_has_no_probe_kernels():
+    """The wrong-by-design bottleneck probes, the first-generation FD kernel and
+    the environment tuning knobs exist only in the probe build (-DNICE_PROBES,
+    `make -C nice_amd probe`); the shipped library contains none of them."""
+    import subprocess
+    syms = subprocess.run(["nm", "-C", _lib.LIB_PATH], capture_output=True, text=True,
+                          check=True).stdout
+    cfgs = re.findall(r"fd2_kernel<nice::fd2::Cfg<(\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (\d+)>", syms)
+    assert cfgs, "no fd2 kernels found"
+    assert all(c[4] == "0" for c in cfgs), "probe instantiation in the product library"
+    assert "detailed_fd_kernel" not in syms
+    with open(_lib.LIB_PATH, "rb") as f:
+        blob = f.read()
+    for knob in (b"NICE_FD2_PROBE", b"NICE_MSD_PROBE", b"NICE_FD_VARIANT", b"NICE_FD2_TCHUNK",
+                 b"NICE_FD2_MINCHUNK", b"NICE_FD2_WG512", b"NICE_MSD_TRACE"):
+        assert knob not in blob, knob

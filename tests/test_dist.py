@@ -58,14 +58,14 @@ def _oracle_detailed_shard(s, e, base):
     return hist, list(r.nice_numbers)
 
 
-def _oracle_niceonly_shard(s, e, base, chunk):
+def _oracle_niceonly_shard(s, e, base, chunk_size, deal_stride=1, deal_offset=0):
+    """The oracle over the chunks nice_process_range_niceonly_ex processes
+    with these deal options (every deal_stride-th chunk of [s, e)'s grid)."""
     from oracle import oracle as O
+    from nice_amd.dist import dealt_chunks
     out = []
-    a = s
-    while a < e:
-        b = min(e, a + chunk)
+    for a, b in dealt_chunks(s, e, chunk_size, deal_stride or 1, deal_offset):
         out += [n for n, _ in O.process_range_niceonly(a, b, base)[0].nice_numbers]
-        a = b
     return out
 
 
@@ -73,10 +73,13 @@ class _OracleCtx:
     """Stands in for nice_amd.GpuContext in the CPU tests (oracle-backed)."""
 
     def detailed_raw(self, s, e, base):
+        assert s < e, "empty detailed shard must not reach the library"
         return _oracle_detailed_shard(s, e, base)
 
-    def niceonly_raw(self, s, e, base, chunk_size=0, **_):
-        return _oracle_niceonly_shard(s, e, base, chunk_size), None
+    def niceonly_raw(self, s, e, base, chunk_size=0, deal_stride=1, deal_offset=0, **_):
+        from nice_amd.dist import client_chunk_size
+        return _oracle_niceonly_shard(s, e, base, chunk_size or client_chunk_size(e - s),
+                                      deal_stride, deal_offset), None
 
 
 def _field_worker(rank, world, port, q):
@@ -120,6 +123,15 @@ def _field_worker(rank, world, port, q):
     res["pipelined_both"] = [([(d.num_uniques, d.count) for d in r[0].distribution],
                               [(n.number, n.num_uniques) for n in r[0].nice_numbers],
                               [n.number for n in r[1].nice_numbers]) for r in got[1:]]
+    # a field smaller than the world: rank 1's detailed shard is empty and
+    # must contribute zeros instead of calling the library (no hang)
+    r = D.process_range_detailed_dist(FieldSize(69, 70), 10, shard_fn=_oracle_detailed_shard)
+    res["tiny"] = ([(d.num_uniques, d.count) for d in r.distribution],
+                   [(n.number, n.num_uniques) for n in r.nice_numbers])
+    det, nic, _ = D.process_field_both_dist(FieldSize(69, 70), 10, _OracleCtx())
+    res["tiny_both"] = ([(d.num_uniques, d.count) for d in det.distribution],
+                        [(n.number, n.num_uniques) for n in det.nice_numbers],
+                        [n.number for n in nic.nice_numbers])
     q.put((rank, res))
     dist.destroy_process_group()
 
@@ -155,8 +167,15 @@ def test_two_rank_field_sharding_matches_single_process():
         assert r == (w.distribution, w.nice_numbers, _oracle_niceonly_shard(a, a + 2_000, 10, 997))
     assert out[0]["pipelined"][0][2] == [69]
     assert out[0]["pipelined_both"] == out[0]["pipelined"]
-    # shard cuts fall on the whole field's chunk grid
-    assert D.shard_bounds(0, 10 ** 6, 0, 2, 99_991)[1] % 99_991 == 0
+    w = O.process_range_detailed(69, 70, 10)
+    assert out[0]["tiny"] == (w.distribution, [(69, 10)])
+    assert out[0]["tiny_both"] == (w.distribution, [(69, 10)], [69])
+    # niceonly is dealt on the whole field's chunk grid
+    from nice_amd.types import FieldSize
+    assert D.niceonly_deal(FieldSize(0, 10 ** 6), 1, 2, 99_991) == \
+        {"chunk_size": 99_991, "deal_stride": 2, "deal_offset": 1}
+    assert D.niceonly_deal(FieldSize(0, 5), 1, 2) is None
+    assert list(D.dealt_chunks(0, 10, 3, 2, 1)) == [(3, 6), (9, 10)]
     assert D.shard_bounds(0, 10, 1, 3) == (4, 7)
     assert D.client_chunk_size(10 ** 9) == 10 ** 6 and D.client_chunk_size(10 ** 13) == 10 ** 8
 
@@ -185,3 +204,35 @@ def test_both_modes_runner_matches_sequential_and_propagates_errors():
         bad.close()
     finally:
         both.close()
+
+
+def test_niceonly_dealing_balances_survival_skew():
+    """Per-rank niceonly work under dealing (dist.niceonly_deal), on a scaled
+    b50 window across the massive field's survival onset (the MSD filter
+    prunes everything before it): with 8 ranks every rank's candidate count
+    is within 10 % of the mean, while contiguous slabs would give rank 0
+    almost nothing; the dealt chunks together are the single-process run."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from nice_amd import dist as D
+    from nice_amd.types import FieldSize
+    from oracle import oracle as O
+    a = O.base_range(50)[0] + 7_372_000_000_000
+    e, chunk, world = a + 2 * 10 ** 9, 10 ** 6, 8
+
+    def cands(c):
+        return O.process_field_niceonly_ex(c[0], c[1], 50, 1, chunk=chunk)[1]
+
+    with ThreadPoolExecutor(8) as pool:
+        per_rank = []
+        for r in range(world):
+            deal = D.niceonly_deal(FieldSize(a, e), r, world, chunk)
+            per_rank.append(sum(pool.map(cands, D.dealt_chunks(a, e, **{
+                "chunk": deal["chunk_size"], "stride": deal["deal_stride"],
+                "offset": deal["deal_offset"]}))))
+        slabs = [sum(pool.map(cands, D.dealt_chunks(*D.shard_bounds(a, e, r, world, chunk),
+                                                    chunk, 1, 0))) for r in (0,)]
+    mean = sum(per_rank) / world
+    assert all(abs(c - mean) <= 0.1 * mean for c in per_rank), per_rank
+    assert slabs[0] < 0.01 * mean  # the contiguous first slab is pruned
+    assert sum(per_rank) == O.process_field_niceonly_ex(a, e, 50, 8, chunk=chunk)[1]

@@ -122,23 +122,6 @@ def test_fd_kernel_limb_count_cuts(ctx, base):
         check_detailed(ctx, c - 1, c + 2, base)
 
 
-def test_fd_kernel_generations_agree(ctx):
-    """The production FD kernel and the first-generation FD kernel
-    (NICE_FD_VARIANT=1) give identical results on large in-range fields."""
-    import os
-    for base, size in ((40, 3 * 10 ** 8), (50, 10 ** 8), (80, 5 * 10 ** 7)):
-        s, e = O.base_range(base)
-        a = s + (e - s) // 2
-        want = ctx.detailed_raw(a, a + size, base)
-        os.environ["NICE_FD_VARIANT"] = "1"
-        try:
-            got = ctx.detailed_raw(a, a + size, base)
-        finally:
-            os.environ["NICE_FD_VARIANT"] = "0"
-        assert got == want, base
-        assert sum(want[0]) == size
-
-
 def test_fd_kernel_random_windows(ctx):
     rng = random.Random(7)
     for base in (40, 50, 80):
