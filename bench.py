@@ -1,21 +1,32 @@
 #!/usr/bin/env python3
-"""Benchmark: numbers checked/sec per node, detailed + niceonly, 1e9 @ base 40
+"""Benchmark: numbers checked/sec per node, detailed+niceonly, 1e9 @ base 40
 (BASELINE.json metric; benchmark.rs:60 ExtraLarge field).
 
 One step = one pass of the hot path over one field in BOTH modes: a detailed
 pass (histogram + near-misses) and a niceonly pass (MSD filter + stride
 candidates), what the reference client does per field in either mode
-(client/src/main.rs:120-208, process_range_*_gpu).  The two passes run at once
-on two HIP streams of the GPU (nice_amd.BothModes; --sequential runs them one
-after the other).  Inputs are the field bounds only (no host buffers): the
-kernels derive every n themselves.
+(client/src/main.rs:120-208, process_range_*_gpu).  Inputs are the field
+bounds only (no host buffers): the kernels derive every n themselves.
 
-Multi-GPU (one process per GPU, torchrun): weak scaling -- N GPUs process one
-N x 1e9 field of base 40, [start, start + N*1e9); rank r takes the r-th
-contiguous 1e9 shard (nice_amd/dist.py).  Per step the shard histograms are
-combined with one RCCL all-reduce (base + 1 u64 bins) and the near-miss / nice
-lists are all-gathered, so every rank ends the step holding the whole field's
-results -- the north star's exchange, inside the timed region.
+Fields are pipelined (nice_amd.dist.FieldPipeline): each step submits its
+field to the GPU -- detailed on one stream, niceonly on a second -- before the
+previous field's results are collected, so the GPU never waits for the host
+between steps.  Every field's results come back and are checked (histogram
+mass = field size); the last ones are collected inside the timed region.
+`--sync` runs the synchronous library calls instead (both modes at once on two
+streams, nice_amd.BothModes; no cross-field overlap).
+
+Multi-GPU (one process per GPU, torchrun; --scaling, default strong):
+  strong  the ONE 1e9 field of the metric is split N ways: rank r takes the
+          r-th contiguous detailed shard and is dealt every N-th niceonly chunk
+          of the field's chunk grid (nice_amd/dist.py);
+  weak    N GPUs process one N x 1e9 field, split the same way.
+Per step the shard histograms and list lengths are combined with one RCCL
+all-reduce (overlapped with the next step's compute) and the near-miss / nice
+lists are all-gathered when non-empty, so every rank ends holding the whole
+field's results -- the north star's exchange, inside the timed region.  Under
+strong scaling rank 0 then times the whole field alone on its GPU (the other
+ranks wait) and reports strong_efficiency = T1 / (N * T_N) from the same run.
 Timing: barrier + device sync on both sides of exactly K steps, max over ranks.
 
     python bench.py [--gpus N --steps K --warmup W] [--no-cpu-baseline]
@@ -29,19 +40,24 @@ import sys
 import time
 
 # Hardware queues per process (HIP's default is 4): torch's stream, RCCL's
-# stream and the two mode streams of BothModes must not share a queue, or the
-# niceonly pass serialises behind the detailed kernel (torchrun 1 rank: 2.86
-# ms per step with 4 queues, 2.61 with 8).  Set before HIP initialises; an
-# exported value below 8 (the box exports HIP's default, 4) is raised.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+# stream and the two mode streams must not share a queue, or the niceonly
+# pass serialises behind the detailed kernel (torchrun 1 rank, r01: 2.86 ms
+# per step with 4 queues, 2.61 with 8).  Set before HIP initialises; an
+# exported value below 8 (the box exports HIP's default, 4) is raised, and the
+# value used is recorded in the JSON line's config.
+HW_QUEUES_EXPORTED = os.environ.get("GPU_MAX_HW_QUEUES")
+if int(HW_QUEUES_EXPORTED or 0) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+PROBE_LIB = "--probe-lib" in sys.argv  # A/B experiments only (scripts/probe_lib.py)
+if PROBE_LIB:
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import probe_lib  # noqa: E402,F401
 
 FIELD_SIZE = 10 ** 9
 BASE = 40
-W_ALG = 4 * BASE                    # int32 VALU ops per n
 PEAK_INT32_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 78.64 Tops/s per MI355X (MI355X_MICROARCH.md)
 
 
@@ -54,18 +70,27 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="target CPU work for the bounded cpu_baseline sample")
     p.add_argument("--mode", choices=["both", "detailed", "niceonly"], default="both")
+    p.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                   help="N > 1: split the one 1e9 field N ways (strong) or run an N x 1e9 field (weak)")
+    p.add_argument("--base", type=int, default=BASE, help="(config lines) base of the field")
+    p.add_argument("--field-size", type=float, default=FIELD_SIZE, help="(config lines) field size")
     p.add_argument("--msd-floor", type=int, default=0, help="0 = reference CPU-path floor 250")
     p.add_argument("--msd-where", choices=["auto", "host", "device"], default="auto",
                    help="niceonly MSD filter placement (same candidate set either way)")
-    p.add_argument("--sequential", action="store_true",
-                   help="run the two modes one after the other on one stream (default: at once, "
-                        "on two streams of the GPU, nice_amd.BothModes)")
+    p.add_argument("--depth", type=int, default=2, choices=[1, 2],
+                   help="fields kept in flight behind the one being collected")
+    p.add_argument("--probe-lib", action="store_true",
+                   help="A/B experiments: load the probe build (env tuning knobs live only there)")
+    p.add_argument("--two-ctx", action="store_true",
+                   help="A/B: detailed and niceonly on separate contexts")
+    p.add_argument("--sync", action="store_true",
+                   help="synchronous library calls (no cross-field pipelining)")
     return p.parse_args()
 
 
 def pmc_traffic():
     """HBM bytes per main launch of the detailed kernel, from the committed PMC
-    pass (scripts/gpu_pmc.sh -> profiles/r01/traffic.json); None if absent."""
+    pass (profiles/r01/traffic.json); None if absent."""
     p = os.path.join(ROOT, "profiles", "r01", "traffic.json")
     try:
         with open(p) as f:
@@ -74,16 +99,17 @@ def pmc_traffic():
         return None
 
 
-def rank_field(base_start: int, rank: int):
-    """Weak scaling: rank r owns the r-th consecutive 1e9 field of base 40."""
-    start = base_start + rank * FIELD_SIZE
-    return start, start + FIELD_SIZE
+def rank_field(base_start: int, rank: int, size: int = FIELD_SIZE):
+    """Rank r's 1e9 shard of an N x 1e9 weak-scaling field (kept for the
+    plumbing tests; the pipeline computes shards itself)."""
+    start = base_start + rank * size
+    return start, start + size
 
 
 def timed(step, steps: int, sync, dist=None, tail=None):
     """Barrier + device sync on both sides of exactly `steps` steps (plus
-    `tail`, e.g. collecting the last step's overlapped exchange); returns the
-    max elapsed seconds over ranks (all_reduce MAX)."""
+    `tail`, e.g. collecting the pipeline's last fields); returns the max
+    elapsed seconds over ranks (all_reduce MAX)."""
     sync()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -101,11 +127,21 @@ def timed(step, steps: int, sync, dist=None, tail=None):
     return elapsed
 
 
-def cpu_threads():
-    for k in ("OMP_NUM_THREADS", "MAX_JOBS"):
-        if os.environ.get(k, "").isdigit():
-            return max(1, int(os.environ[k]))
-    return max(1, min(16, os.cpu_count() or 1))
+def cpu_share() -> tuple:
+    """CPUs this process may actually use: the cgroup CPU quota (the GPU box
+    grants 16 per GPU through cpu.max while os.cpu_count() shows every logical
+    CPU of the host), else the affinity mask.  Returns (cpus, how)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()
+        if quota != "max":
+            return max(1, int(int(quota) // int(period))), "cgroup cpu.max quota"
+    except (OSError, ValueError):
+        pass
+    try:
+        return len(os.sched_getaffinity(0)), "affinity mask"
+    except AttributeError:
+        return os.cpu_count() or 1, "os.cpu_count"
 
 
 def cpu_model() -> str:
@@ -119,45 +155,47 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(start, target_s):
-    """Reference algorithm (oracle/ C restatement, 'port') on the host cores,
-    on a bounded sample of the same workload, extrapolated per number."""
+def cpu_baseline(start, target_s, base=BASE, field=FIELD_SIZE):
+    """Reference algorithm (oracle/ C restatement, 'port') on every CPU the
+    box grants this process, on a bounded sample of the same workload: the
+    detailed leg on the first n of the field (sized to ~target_s, per-number
+    rate extrapolated to the field), the niceonly leg on the whole field."""
     from oracle import oracle as O
-    th = cpu_threads()
-    # detailed: size the sample to ~target_s of work
+    th, how = cpu_share()
     probe = 4_000_000
     t = time.perf_counter()
-    O.process_field_detailed_mt(start, start + probe, BASE, th)
+    O.process_field_detailed_mt(start, start + probe, base, th)
     rate = probe / (time.perf_counter() - t)
-    n = int(min(FIELD_SIZE, max(probe, rate * target_s)))
+    n = int(min(field, max(probe, rate * target_s)))
     n = max(1_000_000, n // 1_000_000 * 1_000_000)
     t = time.perf_counter()
-    O.process_field_detailed_mt(start, start + n, BASE, th)
+    O.process_field_detailed_mt(start, start + n, base, th)
     td = time.perf_counter() - t
     det_rate = n / td
-    # niceonly: the whole field (the MSD filter skips most of it at this start)
     t = time.perf_counter()
-    O.process_field_niceonly_mt(start, start + FIELD_SIZE, BASE, th)
+    O.process_field_niceonly_mt(start, start + field, base, th)
     tn = time.perf_counter() - t
-    nice_rate = FIELD_SIZE / tn
-    combined = 2 * FIELD_SIZE / (FIELD_SIZE / det_rate + tn)
+    nice_rate = field / tn
+    combined = 2 * field / (field / det_rate + tn)
     # the reference client's default thread count (--threads 4,
     # client/src/main.rs:94), on a smaller detailed sample
     n4 = max(1_000_000, int(det_rate / th * 4 * target_s / 3) // 1_000_000 * 1_000_000)
     t = time.perf_counter()
-    O.process_field_detailed_mt(start, start + n4, BASE, 4)
+    O.process_field_detailed_mt(start, start + n4, base, 4)
     det4 = n4 / (time.perf_counter() - t)
     t = time.perf_counter()
-    O.process_field_niceonly_mt(start, start + FIELD_SIZE, BASE, 4)
+    O.process_field_niceonly_mt(start, start + field, base, 4)
     tn4 = time.perf_counter() - t
     return {"value": combined, "unit": "numbers/s", "cores": th, "kind": "port",
+            "nproc": th, "cores_source": how, "host_logical_cpus": os.cpu_count(),
             "cpu_model": cpu_model(),
-            "threads4": {"value": 2 * FIELD_SIZE / (FIELD_SIZE / det4 + tn4), "cores": 4,
-                         "detailed_numbers_per_sec": det4, "niceonly_numbers_per_sec": FIELD_SIZE / tn4,
-                         "sample": f"detailed: first {n4:.3g} n; niceonly: whole 1e9 field"},
-            "sample": f"detailed: first {n:.3g} n of the field on {th} threads "
-                      f"({det_rate:.3e} n/s, extrapolated to 1e9); niceonly: whole 1e9 field "
-                      f"({nice_rate:.3e} n/s); reference client chunking, MSD floor 250, k=2",
+            "threads4": {"value": 2 * field / (field / det4 + tn4), "cores": 4,
+                         "detailed_numbers_per_sec": det4, "niceonly_numbers_per_sec": field / tn4,
+                         "sample": f"detailed: first {n4:.3g} n; niceonly: whole field"},
+            "sample": f"detailed: first {n:.3g} n of the field on {th} threads ({td:.1f} s, "
+                      f"{det_rate:.3e} n/s, extrapolated per number to {field:.0e}); niceonly: "
+                      f"whole field ({tn:.1f} s, {nice_rate:.3e} n/s); reference client "
+                      f"chunking, MSD floor 250, k=2",
             "detailed_numbers_per_sec": det_rate, "niceonly_numbers_per_sec": nice_rate}
 
 
@@ -166,6 +204,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    base, field_size = args.base, int(args.field_size)
+    w_alg = 4 * base                    # int32 VALU ops per n
     dist = None
     # The JSON line is the only thing on stdout: runtime banners (RCCL prints
     # its version block to fd 1 when the communicator comes up) go to stderr.
@@ -180,111 +220,135 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import nice_amd as N
+    from nice_amd import dist as D
 
-    ctx = N.GpuContext([local])
-    # Both modes of a field at once: niceonly's launch-bound MSD levels run on
-    # a second stream beside the detailed kernel (nice_amd.BothModes).
-    runner = N.BothModes(local, det_ctx=ctx) if args.mode == "both" and not args.sequential else ctx
-    br = N.get_base_range_u128(BASE)
-    start, end = rank_field(br.range_start, rank)
-    assert end <= br.range_end
+    br = N.get_base_range_u128(base)
+    strong = args.scaling == "strong" or world == 1
+    job_size = field_size if strong else field_size * world
+    field = N.FieldSize(br.range_start, br.range_start + job_size)
+    assert field.range_end <= br.range_end
+    # One context runs both modes: per in-flight field a detailed stream and a
+    # high-priority niceonly stream (the MSD chain of short dependent launches
+    # cuts in ahead of queued detailed workgroups).  --sync uses two contexts.
+    det_ctx = N.GpuContext([local])
+    nice_ctx = N.GpuContext([local]) if args.sync or args.two_ctx else det_ctx
+    nice_opts = {"msd_floor": args.msd_floor, "msd_where": args.msd_where}
+    modes = {"both": (True, True), "detailed": (True, False), "niceonly": (False, True)}[args.mode]
 
     def barrier_sync():
-        # Every library call is synchronous (it returns host results), so the
-        # device is idle here; the torch sync/barrier line the ranks up.
         if dist is not None:
             import torch
             torch.cuda.synchronize()
             dist.barrier()
             torch.cuda.synchronize()
 
-    det_ms, nice_ms, kern_ms, both_ms = [], [], [], []
-    last_nice_stats = None
-    from nice_amd import dist as D
-    whole = N.FieldSize(br.range_start, br.range_start + world * FIELD_SIZE)
-    ex = D.PipelinedExchange(dist) if dist is not None else None
+    last_stats = [None]
 
-    def check_both(done):
-        nonlocal last_nice_stats
-        if done is None:
-            return
-        det, _, st = done
-        last_nice_stats = st or last_nice_stats
-        assert sum(d.count for d in det.distribution) == FIELD_SIZE * world
+    def check(res):
+        _, det, _, st = res
+        if modes[0]:
+            assert sum(d.count for d in det.distribution) == job_size
+        last_stats[0] = st or last_stats[0]
 
-    def step():
-        nonlocal last_nice_stats
-        if dist is not None and args.mode == "both":
-            # both modes of the rank's shard, then ONE all-reduce, overlapped
-            # with the next step's compute (nice_amd/dist.py PipelinedExchange);
-            # the previous step's results come back here and are checked.
-            t = time.perf_counter()
-            done = D.process_field_both_pipelined(ex, whole, BASE, runner, msd_floor=args.msd_floor,
-                                                  msd_where=args.msd_where)
-            det_ms.append((time.perf_counter() - t) * 1e3)
-            kern_ms.append(ctx.kernel_stats().kernel_ms)
-            check_both(done)
-            return
-        if runner is not ctx and dist is None:
-            # single GPU, both modes at once: one wall time for the pair
-            t = time.perf_counter()
-            (hist, _), (_, st) = runner.both_raw((start, end), (start, end), BASE,
-                                                 msd_floor=args.msd_floor, msd_where=args.msd_where)
-            both_ms.append((time.perf_counter() - t) * 1e3)
-            kern_ms.append(ctx.kernel_stats().kernel_ms)
-            assert sum(hist) == FIELD_SIZE
-            last_nice_stats = st
-            return
-        if args.mode in ("both", "detailed"):
-            t = time.perf_counter()
+    def make_pipeline(d):
+        # detailed-only / niceonly-only runs pass a context that skips the other mode
+        return D.FieldPipeline(det_ctx if modes[0] else _Skip(), nice_ctx if modes[1] else _Skip(),
+                               d, depth=args.depth, **nice_opts)
+
+    if args.sync:
+        runner = N.BothModes(local, det_ctx=det_ctx, nice_ctx=nice_ctx)
+        ex = D.PipelinedExchange(dist) if dist is not None else None
+        kern = []
+
+        def step():
             if dist is None:
-                hist, lst = ctx.detailed_raw(start, end, BASE)
-                mass = sum(hist)
+                (hist, _), (_, st) = runner.both_raw(
+                    (field.range_start, field.range_end) if modes[0] else None,
+                    (field.range_start, field.range_end) if modes[1] else None, base, **nice_opts)
+                kern.append(det_ctx.kernel_stats().kernel_ms)
+                if modes[0]:
+                    assert sum(hist) == job_size
+                last_stats[0] = st or last_stats[0]
             else:
-                r = D.process_range_detailed_dist(whole, BASE, ctx=ctx)
-                mass = sum(d.count for d in r.distribution)
-            det_ms.append((time.perf_counter() - t) * 1e3)
-            kern_ms.append(ctx.kernel_stats().kernel_ms)
-            assert mass == FIELD_SIZE * world
-        if args.mode in ("both", "niceonly"):
-            t = time.perf_counter()
-            if dist is None:
-                _, st = ctx.niceonly_raw(start, end, BASE, msd_floor=args.msd_floor,
-                                         msd_where=args.msd_where)
-            else:
-                def shard(s, e, b, chunk):
-                    nonlocal st
-                    lst, st = ctx.niceonly_raw(s, e, b, chunk_size=chunk, msd_floor=args.msd_floor,
-                                               msd_where=args.msd_where)
-                    return lst
-                st = None
-                D.process_range_niceonly_dist(whole, BASE, shard_fn=shard)
-            nice_ms.append((time.perf_counter() - t) * 1e3)
-            last_nice_stats = st
+                done = D.process_field_both_pipelined(ex, field, base, runner, **nice_opts)
+                kern.append(det_ctx.kernel_stats().kernel_ms)
+                if done is not None:
+                    check((field,) + tuple(done))
 
-    def drain():
-        if ex is not None:
-            check_both(D.finish_both(ex, ex.drain()))
+        def tail():
+            if ex is not None:
+                done = D.finish_both(ex, ex.drain())
+                if done is not None:
+                    check((field,) + tuple(done))
+        kernel_ms = kern
+    else:
+        pipe = make_pipeline(dist)
+
+        def step():
+            r = pipe.step(field, base)
+            if r is not None:
+                check(r)
+
+        def tail():
+            for r in pipe.drain():
+                check(r)
+        kernel_ms = pipe.kernel_ms
 
     for _ in range(args.warmup):
         step()
-    drain()
-    det_ms.clear(), nice_ms.clear(), kern_ms.clear(), both_ms.clear()
+    tail()
+    kernel_ms.clear()
 
-    elapsed = timed(step, args.steps, barrier_sync, dist, tail=drain)
+    elapsed = timed(step, args.steps, barrier_sync, dist, tail=tail)
+    pipelined_kms = sum(kernel_ms) / len(kernel_ms) if kernel_ms else None
 
-    modes = 2 if args.mode == "both" else 1
-    total_numbers = modes * FIELD_SIZE * world * args.steps
-    value = total_numbers / elapsed
+    # Roofline phase: in the pipeline consecutive fields' kernels overlap on
+    # two streams (that is the point), so a launch's event span includes its
+    # neighbours'.  The dominant kernel's duration is measured here on its
+    # own: this rank's detailed shard, launched back to back with the host
+    # waiting in between (no overlap), HIP events on the launch stream.
+    iso_ms = []
+    if modes[0]:
+        s_r, e_r = D.shard_bounds(field.range_start, field.range_end, rank, world)
+        for _ in range(max(3, min(10, args.steps))):
+            hist, _ = det_ctx.detailed_raw(s_r, e_r, base)
+            assert sum(hist) == e_r - s_r
+            iso_ms.append(det_ctx.kernel_stats().kernel_ms)
+    kms = sorted(iso_ms)[len(iso_ms) // 2] if iso_ms else None
+
+    # Strong scaling: the whole field on rank 0's GPU alone, same run (T1).
+    t1 = None
+    if dist is not None and strong and world > 1:
+        if rank == 0:
+            solo = make_pipeline(None)
+
+            def solo_step():
+                r = solo.step(field, base)
+                if r is not None:
+                    check(r)
+
+            def solo_tail():
+                for r in solo.drain():
+                    check(r)
+            for _ in range(args.warmup):
+                solo_step()
+            solo_tail()
+            t1 = timed(solo_step, args.steps, lambda: __import__("torch").cuda.synchronize(),
+                       None, tail=solo_tail) / args.steps
+        dist.barrier()
+
+    nmodes = int(modes[0]) + int(modes[1])
+    value = nmodes * job_size * args.steps / elapsed
     if rank != 0:
-        if runner is not ctx:
+        if args.sync:
             runner.close()
-        if dist is not None:
-            dist.destroy_process_group()
+        dist.destroy_process_group()
         return
 
+    default_cfg = base == BASE and field_size == FIELD_SIZE
     line = {
-        "metric": "numbers checked/sec per node, detailed+niceonly, 1e9 @ base 40 field",
+        "metric": "numbers checked/sec per node, detailed+niceonly, 1e9 @ base 40 field"
+        if default_cfg else f"numbers checked/sec per node, {args.mode}, {field_size:.0e} @ base {base} field",
         "value": value,
         "unit": "numbers/s",
         "n_gpus": world,
@@ -292,63 +356,76 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (the reference's deterministic benchmark field; n derived on device)",
         "config": {
-            "workload": "extra-large: 1e9 @ base 40, detailed + niceonly per step "
-                        "(benchmark.rs:60); N GPUs: one N x 1e9 field, rank r takes the r-th "
-                        "1e9 shard, histogram all-reduce + list all-gather per step",
-            "base": BASE, "field_start": start - rank * FIELD_SIZE, "field_size": FIELD_SIZE,
-            "mode": args.mode,
+            "workload": (f"extra-large: {field_size:.0e} @ base {base}, detailed + niceonly per step "
+                         f"(benchmark.rs:60)" if default_cfg else
+                         f"{field_size:.0e} @ base {base}, {args.mode} per step") +
+                        (f"; ONE field sharded {world} ways (rank r: r-th contiguous detailed shard, "
+                         f"every {world}-th niceonly chunk), histogram all-reduce + list all-gather "
+                         f"per step" if world > 1 and strong else
+                         f"; one {world} x field, split {world} ways" if world > 1 else ""),
+            "base": base, "field_start": field.range_start, "field_size": field_size,
+            "job_numbers_per_step": job_size, "mode": args.mode,
             "niceonly_msd_floor": args.msd_floor or 250,
             "niceonly_msd_where": args.msd_where,
             "niceonly_chunking": "reference client (1e6 * clamp(ceil(size/1e11),1,1000))",
-            "parallelism": f"weak{world}",
+            "parallelism": f"{'strong' if strong else 'weak'}{world}",
+            "pipelined": not args.sync,
+            "pipeline_depth": None if args.sync else args.depth,
+            "probe_lib": PROBE_LIB,
+            "gpu_max_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
+            "gpu_max_hw_queues_exported": HW_QUEUES_EXPORTED,
         },
     }
-    if dist is not None and args.mode == "both":
-        line["rank_step_ms"] = sum(det_ms) / len(det_ms)  # both modes + exchange, rank 0
-        line["rank_step_ms_median"] = sorted(det_ms)[len(det_ms) // 2]
-        det_ms.clear()  # not split per mode on this path
-        line["detailed_kernel_ms"] = sum(kern_ms) / len(kern_ms)
-    if kern_ms:
-        kms = sum(kern_ms) / len(kern_ms)
-        achieved = W_ALG * FIELD_SIZE / (kms / 1e3) / 1e12
+    if t1 is not None:
+        line["t1_ms_per_step"] = t1 * 1e3
+        line["strong_efficiency"] = t1 / (world * elapsed / args.steps)
+    if kms is not None and modes[0]:
+        shard = job_size // world
+        achieved = w_alg * shard / (kms / 1e3) / 1e12
+        step_rate = w_alg * shard / (elapsed / args.steps) / 1e12
         line["roofline"] = {
-            "bound": "valu", "kernel": "nice::fd2::fd2_kernel<Cfg<40, 4, 8, 5, 0, 1024>>",
+            "bound": "valu", "kernel": f"nice::fd2::fd2_kernel<Cfg<{base}, ...>>",
             "achieved": achieved, "peak": PEAK_INT32_TOPS, "unit": "int32 Tops/s",
-            "frac": achieved / PEAK_INT32_TOPS, "traffic": pmc_traffic(),
-            "kernel_ms": kms,
-            "work_per_unit": f"{W_ALG} int32 ops per n (4 per digit x {BASE} digits, SURVEY 8d)",
-            "note": "integer-VALU/LDS bound (no HBM stream, no contraction); kernel time from "
-                    "HIP events on the launch stream (main + tail launch of one field); traffic: "
-                    "HBM bytes per launch from the committed PMC pass (profiles/r01/traffic.json, "
-                    "FETCH_SIZE x2 + WRITE_SIZE), the field's bounds are the only input",
+            "frac": achieved / PEAK_INT32_TOPS, "traffic": pmc_traffic() if default_cfg else None,
+            "kernel_ms": kms, "numbers_per_launch": shard,
+            "work_per_unit": f"{w_alg} int32 ops per n (4 per digit x {base} digits, SURVEY 8d)",
+            "pipelined_frac": step_rate / PEAK_INT32_TOPS,
+            "pipelined_launch_span_ms": pipelined_kms,
+            "note": "integer-VALU/LDS bound (no HBM stream, no contraction); kernel_ms = median "
+                    "duration of this rank's detailed shard (main + tail launch) from HIP events "
+                    "on the launch stream, launched back to back without overlap after the timed "
+                    "region; pipelined_frac = the same work per timed step (both modes share "
+                    "the GPU, consecutive fields overlap on two streams); traffic: HBM bytes per "
+                    "launch from the committed PMC pass (profiles/r01/traffic.json, FETCH_SIZE x2 "
+                    "+ WRITE_SIZE), the field's bounds are the only input",
         }
-    line["modes_overlapped"] = runner is not ctx
-    if both_ms:
-        line["both_wall_ms"] = sum(both_ms) / len(both_ms)  # detailed + niceonly at once
-        line["both_wall_ms_median"] = sorted(both_ms)[len(both_ms) // 2]
-    if det_ms:
-        line["detailed_numbers_per_sec"] = FIELD_SIZE / (sum(det_ms) / len(det_ms) / 1e3)
-        line["detailed_ms"] = sum(det_ms) / len(det_ms)
-    if nice_ms:
-        line["niceonly_numbers_per_sec"] = FIELD_SIZE / (sum(nice_ms) / len(nice_ms) / 1e3)
-        line["niceonly_ms"] = sum(nice_ms) / len(nice_ms)
-    st = last_nice_stats
-    if st is not None and (nice_ms or both_ms or dist is not None):
+    st = last_stats[0]
+    if st is not None:
         line["niceonly"] = {"ranges": st.ranges, "range_numbers": st.range_numbers,
                             "candidates": st.candidates, "launches": st.launches,
-                            "msd_seconds": st.msd_seconds, "total_seconds": st.total_seconds}
+                            "rank0_dealt_chunks": f"every {world}-th" if world > 1 else "all"}
     if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(br.range_start, args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(br.range_start, args.cpu_seconds, base, field_size)
     print(json.dumps(line), file=json_out, flush=True)
-    if runner is not ctx:
+    if args.sync:
         runner.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+class _Skip:
+    """A context that runs nothing (single-mode bench runs)."""
+
+    def detailed_submit(self, *a, **k):
+        return None
+
+    def niceonly_submit(self, *a, **k):
+        return None
 
 
 if __name__ == "__main__":

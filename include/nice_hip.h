@@ -130,8 +130,29 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
 int nice_validate_detailed(uint32_t base, uint64_t size_lo, uint64_t size_hi, const uint64_t *hist,
                            const nice_number *list, size_t n);
 
-/* Device time of the hot kernel(s) in the last detailed call on a device,
- * measured with HIP events on the launch stream. */
+/* Asynchronous fields.  *_submit enqueues a field on the context's devices
+ * and returns at once with a ticket; *_collect waits for that field and
+ * returns exactly what the synchronous call would (the synchronous entry
+ * points above are submit + collect).  Up to three fields per mode may be in
+ * flight on a context, each on its own stream, so a caller can keep the GPU
+ * busy with fields i+1 and i+2 while it exchanges / submits the results of
+ * field i -- the overlap the reference client gets from its pipelined loop
+ * (client/src/main.rs:411-562) -- and a field's first workgroups fill the CUs
+ * the previous field's last ones leave idle.  Tickets
+ * are collected in any order; NICE_ERR_CAPACITY from a collect keeps the
+ * results for a retry with a larger list.  Niceonly with msd_where = host runs
+ * its host MSD producer inside submit. */
+int nice_detailed_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, uint64_t end_lo,
+                         uint64_t end_hi, uint32_t base, int *ticket);
+int nice_detailed_collect(nice_ctx *ctx, int ticket, uint64_t *hist, nice_number *out, size_t cap,
+                          size_t *n_out);
+int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, uint64_t end_lo,
+                         uint64_t end_hi, uint32_t base, const nice_niceonly_opts *opts, int *ticket);
+int nice_niceonly_collect(nice_ctx *ctx, int ticket, nice_number *out, size_t cap, size_t *n_out,
+                          nice_niceonly_stats *stats);
+
+/* Device time of the hot kernel(s) of the last collected detailed field on a
+ * device, measured with HIP events on the launch stream. */
 typedef struct {
     double kernel_ms;    /* summed over launches */
     uint32_t launches;

@@ -28,7 +28,8 @@ EXPORTS = (
     "nice_gpu_supports_base", "nice_fd_kernel_base", "nice_msd_valid_ranges",
     "nice_msd_skippable", "nice_stride_table", "nice_debug_unique_counts",
     "nice_debug_is_nice", "nice_check_is_nice_inrange", "nice_check_msd_skippable_inrange",
-    "nice_fd_segment_cuts", "nice_validate_detailed",
+    "nice_fd_segment_cuts", "nice_validate_detailed", "nice_detailed_submit",
+    "nice_detailed_collect", "nice_niceonly_submit", "nice_niceonly_collect",
 )
 
 
@@ -118,6 +119,11 @@ def lib():
         "nice_check_msd_skippable_inrange": ([u32, u64, u64, u64, u64], i32),
         "nice_fd_segment_cuts": ([u32, P64, sz, PSZ], i32),
         "nice_validate_detailed": ([u32, u64, u64, P64, PN, sz], i32),
+        "nice_detailed_submit": ([vp, u64, u64, u64, u64, u32, ctypes.POINTER(i32)], i32),
+        "nice_detailed_collect": ([vp, i32, P64, PN, sz, PSZ], i32),
+        "nice_niceonly_submit": ([vp, u64, u64, u64, u64, u32, ctypes.POINTER(nice_niceonly_opts),
+                                  ctypes.POINTER(i32)], i32),
+        "nice_niceonly_collect": ([vp, i32, PN, sz, PSZ, ctypes.POINTER(nice_niceonly_stats)], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

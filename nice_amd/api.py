@@ -182,6 +182,30 @@ class GpuContext:
                    for i in range(n.value)]
             return list(hist), lst
 
+    def detailed_submit(self, start: int, end: int, base: int) -> int:
+        """Enqueue a detailed field and return at once (a ticket for
+        detailed_collect); at most two fields in flight per context."""
+        t = ctypes.c_int()
+        check(lib().nice_detailed_submit(self._h, *_split(start), *_split(end), base, t))
+        return t.value
+
+    def detailed_collect(self, ticket: int, base: int, cap: int = 0):
+        """(hist, near-misses) of a submitted field, as detailed_raw returns."""
+        hist = self._hist.get(base)
+        if hist is None:
+            hist = self._hist[base] = (ctypes.c_uint64 * (base + 1))()
+        cap = max(cap, self._out_cap, 1024)
+        while True:
+            out = self._out_buf(cap)
+            n = ctypes.c_size_t()
+            rc = lib().nice_detailed_collect(self._h, ticket, hist, out, cap, n)
+            if rc == _lib.NICE_ERR_CAPACITY:
+                cap = n.value
+                continue
+            check(rc)
+            return list(hist), [(out[i].number_lo | (out[i].number_hi << 64), out[i].num_uniques)
+                                for i in range(n.value)]
+
     # -- niceonly -------------------------------------------------------------
     def niceonly_raw(self, start: int, end: int, base: int, msd_floor: int = 0,
                      chunk_size: int = 0, threads: int = 0, stride_k: int = 0,
@@ -190,9 +214,8 @@ class GpuContext:
         """Nice numbers of [start, end) ascending, and NiceonlyStats.  With
         deal_stride N > 1 only the field's chunks c with c % N == deal_offset
         are processed (rank deal_offset of an N-way job, nice_amd/dist.py)."""
-        where = {"auto": 0, "host": 1, "device": 2}[msd_where]
-        opts = _lib.nice_niceonly_opts(msd_floor, chunk_size, threads, stride_k, where,
-                                       deal_stride, deal_offset, 0)
+        opts = self._nice_opts(msd_floor, chunk_size, threads, stride_k, msd_where, deal_stride,
+                               deal_offset)
         st = _lib.nice_niceonly_stats()
         cap = max(cap, self._out_cap, 1024)
         while True:
@@ -208,6 +231,37 @@ class GpuContext:
             stats = NiceonlyStats(st.ranges, st.range_numbers, st.candidates, st.launches,
                                   st.msd_seconds, st.total_seconds)
             return lst, stats
+
+    @staticmethod
+    def _nice_opts(msd_floor=0, chunk_size=0, threads=0, stride_k=0, msd_where="auto",
+                   deal_stride=0, deal_offset=0):
+        where = {"auto": 0, "host": 1, "device": 2}[msd_where]
+        return _lib.nice_niceonly_opts(msd_floor, chunk_size, threads, stride_k, where,
+                                       deal_stride, deal_offset, 0)
+
+    def niceonly_submit(self, start: int, end: int, base: int, **opts) -> int:
+        """Enqueue a niceonly field (options as niceonly_raw) and return a
+        ticket for niceonly_collect."""
+        t = ctypes.c_int()
+        check(lib().nice_niceonly_submit(self._h, *_split(start), *_split(end), base,
+                                         self._nice_opts(**opts), t))
+        return t.value
+
+    def niceonly_collect(self, ticket: int, cap: int = 0):
+        """(nice numbers, NiceonlyStats) of a submitted field."""
+        st = _lib.nice_niceonly_stats()
+        cap = max(cap, self._out_cap, 1024)
+        while True:
+            out = self._out_buf(cap)
+            n = ctypes.c_size_t()
+            rc = lib().nice_niceonly_collect(self._h, ticket, out, cap, n, st)
+            if rc == _lib.NICE_ERR_CAPACITY:
+                cap = n.value
+                continue
+            check(rc)
+            return ([out[i].number_lo | (out[i].number_hi << 64) for i in range(n.value)],
+                    NiceonlyStats(st.ranges, st.range_numbers, st.candidates, st.launches,
+                                  st.msd_seconds, st.total_seconds))
 
     # -- both modes of one field ---------------------------------------------
     def both_raw(self, det_range, nice_range, base: int, **nice_opts):

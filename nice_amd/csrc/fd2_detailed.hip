@@ -562,23 +562,88 @@ static hipError_t fd2_tables(hipStream_t s, const uint4 **out) {
     return hipSuccess;
 }
 
+// One launch covers a whole segment: blocks [0, main_blocks) walk `nunits`
+// chunks of `chunk` numbers from `start`; the blocks after them take the
+// < chunk numbers left over, one per lane, from `tail` (same code, chunk 1:
+// every parameter stays wave-uniform, and no second launch is serialised
+// behind the first).  With fin.out set, the launch also finishes the field:
+// the last workgroup to retire sums the kHistCopies histogram copies into
+// the caller's mapped result words and re-zeroes the state block, so a field
+// is ONE launch instead of main + tail + epilogue (under several fields in
+// flight each small launch waited for free CUs: 25-60 us apiece).
+struct Fd2Args {
+    u64 start_lo, start_hi;
+    u64 tail_lo, tail_hi;
+    u32 nunits, chunk;
+    u32 tail_count, main_blocks;
+    u32 cutoff;
+    u64 *hist;          // kHistCopies x 129 bins
+    NumOut out;
+    const uint4 *tabs;
+    FieldFinish fin;    // fin.out_mapped == nullptr: no in-kernel finish
+};
+
+// Last-workgroup finish (see Fd2Args).  smem is reused as scratch (>= 1 KB).
+// Hand-off without any L2 write-back (MI355X_MICROARCH.md, inter-workgroup
+// visibility: agent atomics both sides, the last arriver told by its add's
+// return value): every wave waits for its own histogram atomics
+// (vmcnt(0)), a barrier, ONE agent-scope add per workgroup; the last
+// workgroup reads the copies with agent-scope (sc1) loads.  A __threadfence()
+// here would write back and invalidate the XCD's whole L2 once per
+// workgroup: 12 000 of them made the b40 1e9 field 1.8x slower.
+template <int WG>
+__device__ __forceinline__ void field_finish(const FieldFinish &fin, u64 *hist, u32 *count,
+                                             unsigned char *smem) {
+    __shared__ u32 last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(fin.done, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    unsigned long long *acc = (unsigned long long *)smem;
+    for (u32 b = threadIdx.x; b < 129; b += WG) acc[b] = 0;
+    __syncthreads();
+    for (u32 e = threadIdx.x; e < kHistCopies * 129; e += WG) {
+        const u64 v = __hip_atomic_load(&hist[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v) {
+            atomicAdd(&acc[e % 129], (unsigned long long)v);
+            __hip_atomic_store(&hist[e], (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    for (u32 b = threadIdx.x; b < 129; b += WG) fin.out_mapped[b] = acc[b];
+    if (threadIdx.x == 0) {
+        fin.out_mapped[129] = __hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fin.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 template <class P>
-__device__ __forceinline__ void fd2_body(u64 start_lo, u64 start_hi, u32 nunits, u32 chunk, u32 cutoff,
-                                         u64 *__restrict__ hist_out, NumOut out,
-                                         const uint4 *__restrict__ tabs) {
+__device__ __forceinline__ void fd2_body(const Fd2Args &a) {
     // Static LDS: its address is a compile-time constant, so a lookup is one
     // ds_read with the table offset in the instruction's immediate field.
     __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDS_BYTES];
     u32 *hist = (u32 *)smem;
     u32 *outl = (u32 *)(smem + P::OUTL);
     const u32 tid = threadIdx.x;
+    const NumOut out = a.out;
+    const u32 cutoff = a.cutoff;
+    // main part or tail part of the launch (workgroup-uniform)
+    const bool main_part = blockIdx.x < a.main_blocks;
+    const u64 start_lo = main_part ? a.start_lo : a.tail_lo;
+    const u64 start_hi = main_part ? a.start_hi : a.tail_hi;
+    const u32 nunits = main_part ? a.nunits : a.tail_count;
+    const u32 chunk = main_part ? a.chunk : 1u;
+    const u32 blk = main_part ? blockIdx.x : blockIdx.x - a.main_blocks;
+    const u32 nblk = main_part ? a.main_blocks : gridDim.x - a.main_blocks;
 
     // The tables (built once per device and base in global memory,
     // fd2_tables) are copied in with 16-byte accesses, and the histogram
     // region zeroed: building them here cost ~5 % of a launch of short chunks.
     {
         uint4 *dst = (uint4 *)(smem + P::TB);
-        for (u32 i = tid; i < (u32)(P::TAB_BYTES / 16); i += P::WG) dst[i] = tabs[i];
+        for (u32 i = tid; i < (u32)(P::TAB_BYTES / 16); i += P::WG) dst[i] = a.tabs[i];
         uint4 *h4 = (uint4 *)smem;
         for (u32 i = tid; i < (u32)(P::TB / 16); i += P::WG) h4[i] = make_uint4(0, 0, 0, 0);
     }
@@ -587,9 +652,9 @@ __device__ __forceinline__ void fd2_body(u64 start_lo, u64 start_hi, u32 nunits,
     // Window counters: row u - W0, column tid (u32) or tid mod WG/2 (u16 half).
     const u32 hbase = (P::HP ? tid % P::HROW : tid) * 4;
     const u32 hinc = P::HP && tid >= (u32)P::HROW ? 0x10000u : 1u;
-    const u32 stride = gridDim.x * P::WG;
+    const u32 stride = nblk * P::WG;
     u32 probe_acc = 0;
-    for (u32 unit = blockIdx.x * P::WG + tid; unit < nunits; unit += stride) {
+    for (u32 unit = blk * P::WG + tid; unit < nunits; unit += stride) {
         u64 n0_lo = start_lo, n0_hi = start_hi;
         add_u128(n0_lo, n0_hi, (u64)unit * chunk);
         State<P> st;
@@ -654,7 +719,7 @@ __device__ __forceinline__ void fd2_body(u64 start_lo, u64 start_hi, u32 nunits,
     if constexpr ((P::PROBE & 2) != 0) atomicAdd(&outl[P::W0], probe_acc);  // mass only
     __syncthreads();
     const u32 lane = tid & 63, wave = tid >> 6;
-    hist_out += (blockIdx.x % kHistCopies) * 129;
+    u64 *hist_out = a.hist + (blockIdx.x % kHistCopies) * 129;
     for (u32 row = wave; row < (u32)P::W; row += P::WG / 64) {
         u32 s = 0;
 #pragma unroll
@@ -668,21 +733,16 @@ __device__ __forceinline__ void fd2_body(u64 start_lo, u64 start_hi, u32 nunits,
     }
     if (tid < (u32)P::NBINS && outl[tid])
         atomicAdd((unsigned long long *)&hist_out[tid], (unsigned long long)outl[tid]);
+    if (a.fin.out_mapped) {
+        __syncthreads();  // smem is reused by the finish
+        field_finish<P::WG>(a.fin, a.hist, out.count, smem);
+    }
 }
 
-// Main launch: units of `chunk` numbers.  Tail launch: the < chunk numbers
-// left over, one per lane (its own symbol, so profiles show it apart).
 template <class P>
 __global__ void __launch_bounds__(P::WG) __attribute__((amdgpu_waves_per_eu(P::WPE, P::WPE)))
-fd2_kernel(u64 start_lo, u64 start_hi, u32 nunits, u32 chunk, u32 cutoff, u64 *__restrict__ hist_out,
-           NumOut out, const uint4 *__restrict__ tabs) {
-    fd2_body<P>(start_lo, start_hi, nunits, chunk, cutoff, hist_out, out, tabs);
-}
-template <class P>
-__global__ void __launch_bounds__(P::WG) __attribute__((amdgpu_waves_per_eu(P::WPE, P::WPE)))
-fd2_tail_kernel(u64 start_lo, u64 start_hi, u32 nunits, u32 cutoff, u64 *__restrict__ hist_out,
-                NumOut out, const uint4 *__restrict__ tabs) {
-    fd2_body<P>(start_lo, start_hi, nunits, 1u, cutoff, hist_out, out, tabs);
+fd2_kernel(Fd2Args a) {
+    fd2_body<P>(a);
 }
 
 template <class P>
@@ -741,22 +801,29 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         // b80 1e9 at chunk 2544 took 11.8 ms, at 2545 9.3.
         if (chunk > 1 && chunk % 2 == 0) chunk++;
         if (chunk > P::B) chunk = P::B % 2 ? P::B : P::B - 1;
-        u64 nunits = cnt / chunk;
+        const u64 nunits = cnt / chunk;
         if (nunits > 0xffffffffull) return hipErrorInvalidValue;
-        if (nunits) {
-            const u64 grid = (nunits + P::WG - 1) / P::WG;  // one chunk per lane
-            hipLaunchKernelGGL(kern, dim3((u32)grid), dim3(P::WG), 0, s, q.start_lo,
-                               q.start_hi, (u32)nunits, (u32)chunk, q.cutoff, q.hist, q.out, tabs);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-        }
         const u64 tail = cnt - nunits * chunk;  // < chunk <= B: one number per lane
-        if (tail) {
-            u64 lo = q.start_lo, hi = q.start_hi;
-            add_u128(lo, hi, nunits * chunk);
-            hipLaunchKernelGGL(fd2_tail_kernel<P>, dim3((u32)((tail + P::WG - 1) / P::WG)), dim3(P::WG), 0,
-                               s, lo, hi, (u32)tail, q.cutoff, q.hist, q.out, tabs);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-        }
+        const u64 main_blocks = (nunits + P::WG - 1) / P::WG;  // one chunk per lane
+        const u64 tail_blocks = (tail + P::WG - 1) / P::WG;
+        Fd2Args a{};
+        a.start_lo = q.start_lo;
+        a.start_hi = q.start_hi;
+        a.tail_lo = q.start_lo;
+        a.tail_hi = q.start_hi;
+        add_u128(a.tail_lo, a.tail_hi, nunits * chunk);
+        a.nunits = (u32)nunits;
+        a.chunk = (u32)chunk;
+        a.tail_count = (u32)tail;
+        a.main_blocks = (u32)main_blocks;
+        a.cutoff = q.cutoff;
+        a.hist = q.hist;
+        a.out = q.out;
+        a.tabs = tabs;
+        // the field's finish rides on its last launch
+        a.fin = left == cnt ? q.fin : FieldFinish{nullptr, nullptr};
+        hipLaunchKernelGGL(kern, dim3((u32)(main_blocks + tail_blocks)), dim3(P::WG), 0, s, a);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
         add_u128(q.start_lo, q.start_hi, cnt);
         left -= cnt;
     }
@@ -921,6 +988,7 @@ hipError_t launch_detailed_fd2(const DetailedLaunch &p, int num_cus, hipStream_t
         q.start_lo = (uint64_t)a;
         q.start_hi = (uint64_t)(a >> 64);
         q.count = (uint64_t)(stop - a);
+        q.fin = stop == e ? p.fin : FieldFinish{nullptr, nullptr};  // finish with the last launch
         hipError_t err = fd2::launch_segment(q, t.combos[i], num_cus, s);
         if (err != hipSuccess) return err;
         a = stop;

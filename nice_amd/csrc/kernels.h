@@ -19,6 +19,15 @@ struct NumOut {
 // the host); a workgroup flushes into copy blockIdx.x % kHistCopies.
 constexpr uint32_t kHistCopies = 64;
 
+// In-kernel end of a field (fd2 kernels): the launch's last workgroup sums
+// the histogram copies into out_mapped[0..128] (mapped host memory), writes
+// the near-miss count to out_mapped[129] and re-zeroes copies, count and
+// *done.  out_mapped == nullptr: the caller runs launch_detailed_finish.
+struct FieldFinish {
+    uint64_t *out_mapped;
+    uint32_t *done;
+};
+
 struct DetailedLaunch {
     uint64_t start_lo, start_hi; // first n of the segment
     uint64_t count;              // numbers in the segment
@@ -26,6 +35,7 @@ struct DetailedLaunch {
     uint32_t cutoff;             // near-miss cutoff (number_stats.rs:15-17)
     uint64_t *hist;              // kHistCopies x 129 u64 bins, accumulated
     NumOut out;
+    FieldFinish fin;             // fd2 only; see FieldFinish
 };
 
 // Bases with a finite-difference kernel (valid only for n inside the base's
@@ -54,6 +64,20 @@ struct Leaf {
     uint32_t count;         // candidates in the range
 };
 
+// In-kernel end of a niceonly field (its last candidate launch): the last
+// workgroup copies the MSD counters (device MSD) and the nice count into
+// mapped host memory, so a field needs no copy launches.
+// Every candidate launch ends with its last workgroup re-zeroing the device
+// MSD's per-batch leaf-record count (counters[24]) for the next batch; the
+// field's last launch instead copies the counters and the nice count out and
+// re-zeroes them for the slot's next field (no memset or copy launches).
+struct NiceFinish {
+    uint32_t *msd_mapped;          // 32 words (device MSD field end) or null
+    uint32_t *count_mapped;        // nice count (field end) or null
+    uint32_t *msd_counters;        // device MSD counters, or null (host MSD)
+    uint32_t *done;                // workgroups retired, re-zeroed; null: no epilogue
+};
+
 struct NiceonlyLaunch {
     const Leaf *leaves;
     const uint32_t *n_leaves_dev;  // leaf count on the device (or null: use n_leaves)
@@ -63,6 +87,7 @@ struct NiceonlyLaunch {
     uint32_t base;
     uint32_t in_range;             // every candidate inside the base's valid range
     NumOut out;
+    NiceFinish fin;
 };
 bool niceonly_specialised(uint32_t base);
 hipError_t launch_niceonly(const NiceonlyLaunch &p, int num_cus, hipStream_t s);
@@ -100,13 +125,26 @@ struct MsdLaunch {
     uint32_t R, M;
     uint32_t base;
     uint32_t in_range;            // the batch lies inside the base's valid range
+    uint32_t first_batch;         // init zeroes the field's sticky counters and *nice_count
+    uint32_t *nice_count;
     uint32_t probe;               // probe build only (NICE_MSD_PROBE): 1 no skip test, 2 no leaf stride math
 };
 // A leaf's candidate count is capped at kLeafPiece: longer runs are stored as
 // several leaves, so niceonly_kernel's per-wave sums of 8 leaves fit 32 bits.
 constexpr uint32_t kLeafPiece = 1u << 28;
-// Enqueue the init + 22 level kernels (no host sync).
-hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s);
+// Node of a chunk's fused recursion: offset from the chunk start, size.
+struct ChunkNode {
+    uint32_t off, size;
+};
+constexpr uint32_t kFusedMaxCap = 1u << 14;
+// Nodes per level of a fused chunk recursion (a power of two), or 0 when the
+// chunk needs the level-launch BFS (chunk / floor too large, or chunk >= 2^32).
+uint32_t msd_fused_cap(uint64_t chunk, uint64_t floor_size);
+// Enqueue a batch's MSD recursion (no host sync): with `scratch` (grid x 2 x
+// cap ChunkNodes) ONE fused launch, one workgroup per chunk; otherwise the
+// init + level kernels.
+hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s, ChunkNode *scratch = nullptr,
+                             uint32_t cap = 0, uint32_t grid = 0);
 
 // Diagnostics used by the parity tests: per-n unique counts / nice flags
 // computed by the same device functions the production kernels use.

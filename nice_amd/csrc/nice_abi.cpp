@@ -3,8 +3,14 @@
 // Replaces the reference's CUDA host pipeline (common/src/client_process_gpu.rs):
 // no NVRTC (kernels are AOT code objects), one HIP stream per device, fields
 // sharded across devices as contiguous n-ranges, histograms summed and
-// near-miss / nice lists merged on the host, and a multi-threaded host MSD
-// producer streaming range descriptors to the niceonly kernel.
+// near-miss / nice lists merged on the host, the MSD recursion on the device
+// (or a multi-threaded host producer streaming range descriptors).
+//
+// Fields are processed asynchronously: every device owns kSlots result slots
+// per mode (device state block, mapped result words, output lists, events), so
+// a caller can submit field i+1 before collecting field i and the GPU never
+// waits for the host between fields (nice_*_submit / nice_*_collect).  The
+// synchronous reference-shaped entry points are submit + collect.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -31,13 +37,25 @@ using nice::u128;
 
 namespace {
 
-// Per-device state block: kHistCopies histograms of 129 u64 bins (kernels
+// Per-slot state block: kHistCopies histograms of 129 u64 bins (kernels
 // spread their end-of-launch atomics over the copies: hundreds of workgroups
 // adding to ONE address serialise in L2), then the two list counters.
 constexpr size_t kHistCopies = nice::kHistCopies;
 constexpr size_t kStateBytes = kHistCopies * 129 * 8 + 2 * 4;
+constexpr int kSlots = 3;  // fields in flight per mode and context
 
 thread_local std::string g_err;
+
+// Slots a context rotates through (probe build: NICE_SLOTS limits it, for
+// pipeline-depth experiments).
+inline int slots_used() {
+#ifdef NICE_PROBES
+    static const int n = getenv("NICE_SLOTS") ? std::max(1, std::min(kSlots, atoi(getenv("NICE_SLOTS")))) : kSlots;
+    return n;
+#else
+    return kSlots;
+#endif
+}
 
 int fail(int code, const std::string &msg) {
     g_err = msg;
@@ -68,34 +86,58 @@ struct LeafBuf {
 };
 
 struct MsdBuf {
-    // device MSD: ping-pong level queues, leaf list, counters (kernels.h)
+    // device MSD: ping-pong level queues (or the fused kernel's per-workgroup
+    // queues), leaf list, counters (kernels.h).
     nice::MsdNode *q[2] = {nullptr, nullptr};
+    nice::ChunkNode *scratch = nullptr;
     nice::Leaf *leaves = nullptr;
     uint32_t *counters = nullptr;  // 32 words
-    uint32_t *h_counters = nullptr;  // pinned
     uint32_t q_cap = 0, leaf_cap = 0;
+    uint64_t scratch_nodes = 0;
+    // counters / nice count not known to be zero (first use, or a field that
+    // did not end in the candidate kernel's epilogue)
+    bool dirty = true;
+};
+
+struct ListBuf {
+    uint64_t *n = nullptr;  // (lo, hi) pairs
+    uint32_t *u = nullptr;  // num_uniques (detailed only)
+    uint32_t cap = 0;
+};
+
+// One field in flight on one device: its own stream (consecutive fields run
+// on alternate streams, so field i+1's first workgroups fill the CUs that
+// field i's last ones leave idle), state block, results and MSD buffers.
+struct Slot {
+    hipStream_t stream = nullptr;   // detailed
+    hipStream_t nstream = nullptr;  // niceonly: high priority, so its chain of short,
+                                    // dependent MSD launches is not queued behind the
+                                    // detailed kernels' workgroups
+    uint64_t *d_state = nullptr;  // kHistCopies x 129 bins, then d_count
+    uint32_t *d_count = nullptr;  // detailed list count
+    uint32_t *d_done = nullptr;   // workgroups retired (fd2's in-kernel finish)
+    uint32_t *d_nice_count = nullptr;  // niceonly list count
+    uint64_t *h_fin = nullptr;    // mapped pinned: summed histogram [0..128], near-miss count [129]
+    uint64_t *d_fin = nullptr;    // device view of h_fin
+    ListBuf det, nice;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_done = nullptr, nice_done = nullptr;
+    uint32_t *h_msd = nullptr;    // mapped: MSD counters at the end of a niceonly field
+    uint32_t *h_nice = nullptr;   // mapped: niceonly list count
+    uint32_t *d_msd_mapped = nullptr, *d_nice_mapped = nullptr;  // device views
+    uint32_t *d_nice_done = nullptr;  // workgroups retired (niceonly in-kernel finish)
+    bool dirty = true;            // state block not known to be zero
+    MsdBuf msd;
 };
 
 struct Device {
     int id = 0;
     int num_cus = 0;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_done = nullptr;
-    uint64_t *d_hist = nullptr;   // kHistCopies x 129 bins, then d_count
-    uint32_t *d_count = nullptr;  // list counters [0] detailed, [1] niceonly (inside d_hist's block)
-    uint64_t *d_list_n = nullptr;
-    uint32_t *d_list_u = nullptr;
-    uint32_t list_cap = 0;
-    uint64_t *h_hist = nullptr;   // pinned
-    uint32_t *h_count = nullptr;  // pinned
-    uint64_t *h_fin = nullptr;    // mapped pinned: summed histogram [0..128], near-miss count [129]
-    uint64_t *d_fin = nullptr;    // device view of h_fin
-    bool state_dirty = true;      // d_hist / d_count[0] not known to be zero
+    hipStream_t aux = nullptr;    // self-check recomputes (never behind a queued field); lazily created
+    Slot slot[kSlots];
     std::map<uint32_t, uint32_t *> residues;  // base*8+k -> device residue table
     std::map<uint32_t, uint32_t *> ranks;     // base*8+k -> lower_bound(residues, r), r in [0, M]
     LeafBuf desc[2];
     int desc_next = 0;
-    MsdBuf msd;
     nice_kernel_stats last{};
 };
 
@@ -114,23 +156,53 @@ struct StrideCache {
 };
 StrideCache g_stride;
 
+struct Entry {
+    u128 n;
+    uint32_t u;
+};
+
+// A submitted field, until its results have been handed to the caller.
+struct DetJob {
+    bool active = false, collected = false;
+    u128 s = 0, e = 0;
+    uint32_t base = 0;
+    std::vector<u128> bounds;      // per-device shard bounds
+    std::vector<uint64_t> total;   // merged histogram (after collection)
+    std::vector<Entry> all;        // merged near-miss list (after collection)
+};
+struct NiceJob {
+    bool active = false, collected = false;
+    uint32_t base = 0;
+    bool on_device = false;
+    bool empty = false;            // nothing enqueued (residue-empty base, no chunk dealt)
+    std::vector<char> used;        // devices that ran part of the field
+    nice_niceonly_stats st{};
+    std::chrono::steady_clock::time_point t0;
+    std::vector<Entry> all;
+};
+
 }  // namespace
 
 struct nice_ctx {
     std::vector<Device> devs;
-    std::mutex mu;  // one in-flight field per context (client_process_gpu.rs:196-201)
+    std::mutex mu;  // serialises calls on one context (client_process_gpu.rs:196-201)
+    DetJob det[kSlots];
+    NiceJob nice[kSlots];
+    int det_next = 0, nice_next = 0;
 };
 
 namespace {
 
-int ensure_list(Device &d, uint32_t cap) {
-    if (d.list_cap >= cap) return NICE_OK;
+int ensure_listbuf(Device &d, ListBuf &l, uint32_t cap, bool with_u) {
+    if (l.cap >= cap) return NICE_OK;
     HIPCHK(hipSetDevice(d.id));
-    if (d.d_list_n) HIPCHK(hipFree(d.d_list_n));
-    if (d.d_list_u) HIPCHK(hipFree(d.d_list_u));
-    HIPCHK(hipMalloc(&d.d_list_n, (size_t)cap * 16));
-    HIPCHK(hipMalloc(&d.d_list_u, (size_t)cap * 4));
-    d.list_cap = cap;
+    if (l.n) HIPCHK(hipFree(l.n));
+    if (l.u) HIPCHK(hipFree(l.u));
+    l.n = nullptr;
+    l.u = nullptr;
+    HIPCHK(hipMalloc(&l.n, (size_t)cap * 16));
+    if (with_u) HIPCHK(hipMalloc(&l.u, (size_t)cap * 4));
+    l.cap = cap;
     return NICE_OK;
 }
 
@@ -149,24 +221,60 @@ int ensure_desc(LeafBuf &b, uint32_t cap) {
     return NICE_OK;
 }
 
-int ensure_msd(Device &d, uint32_t q_cap, uint32_t leaf_cap) {
-    MsdBuf &m = d.msd;
-    if (!m.counters) {
-        HIPCHK(hipMalloc(&m.counters, 32 * 4));
-        HIPCHK(hipHostMalloc(&m.h_counters, 32 * 4, hipHostMallocDefault));
+int ensure_msd(Slot &sl, uint32_t q_cap, uint32_t leaf_cap, uint64_t scratch_nodes) {
+    MsdBuf &m = sl.msd;
+    if (!m.counters) HIPCHK(hipMalloc(&m.counters, 32 * 4));
+    if (m.scratch_nodes < scratch_nodes) {
+        HIPCHK(hipStreamSynchronize(sl.nstream));
+        if (m.scratch) HIPCHK(hipFree(m.scratch));
+        HIPCHK(hipMalloc(&m.scratch, scratch_nodes * sizeof(nice::ChunkNode)));
+        m.scratch_nodes = scratch_nodes;
     }
     if (m.q_cap < q_cap) {
+        // this slot's previous field may still be reading the old queues
+        HIPCHK(hipStreamSynchronize(sl.nstream));
         for (auto &q : m.q)
             if (q) HIPCHK(hipFree(q));
         for (auto &q : m.q) HIPCHK(hipMalloc(&q, (size_t)q_cap * sizeof(nice::MsdNode)));
         m.q_cap = q_cap;
     }
     if (m.leaf_cap < leaf_cap) {
+        HIPCHK(hipStreamSynchronize(sl.nstream));
         if (m.leaves) HIPCHK(hipFree(m.leaves));
         HIPCHK(hipMalloc(&m.leaves, (size_t)leaf_cap * sizeof(nice::Leaf)));
         m.leaf_cap = leaf_cap;
     }
     return NICE_OK;
+}
+
+int slot_init(Device &d, Slot &sl) {
+    HIPCHK(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+    int least = 0, greatest = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+#ifdef NICE_PROBES
+    if (getenv("NICE_NICE_PRIO") && atoi(getenv("NICE_NICE_PRIO")) == 0) greatest = least;
+#endif
+    HIPCHK(hipStreamCreateWithPriority(&sl.nstream, hipStreamNonBlocking, greatest));
+    HIPCHK(hipMalloc(&sl.d_nice_count, 4));
+    // hist bins and list counters in one block: one memset per field at most.
+    HIPCHK(hipMalloc(&sl.d_state, kStateBytes));
+    sl.d_count = (uint32_t *)(sl.d_state + kHistCopies * 129);
+    sl.d_done = sl.d_count + 1;
+    HIPCHK(hipHostMalloc(&sl.h_fin, 130 * 8, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void **)&sl.d_fin, sl.h_fin, 0));
+    HIPCHK(hipHostMalloc(&sl.h_msd, 32 * 4, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void **)&sl.d_msd_mapped, sl.h_msd, 0));
+    HIPCHK(hipHostMalloc(&sl.h_nice, 4, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void **)&sl.d_nice_mapped, sl.h_nice, 0));
+    HIPCHK(hipMalloc(&sl.d_nice_done, 4));
+    HIPCHK(hipMemset(sl.d_nice_done, 0, 4));
+    HIPCHK(hipEventCreate(&sl.ev0));
+    HIPCHK(hipEventCreate(&sl.ev1));
+    HIPCHK(hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&sl.nice_done, hipEventDisableTiming));
+    int rc = ensure_listbuf(d, sl.det, kInitialListCap, true);
+    if (!rc) rc = ensure_listbuf(d, sl.nice, kNiceCap, false);
+    return rc;
 }
 
 int device_init(Device &d, int id) {
@@ -175,26 +283,21 @@ int device_init(Device &d, int id) {
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, id));
     d.num_cus = prop.multiProcessorCount;
-    HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-    HIPCHK(hipEventCreate(&d.ev0));
-    HIPCHK(hipEventCreate(&d.ev1));
-    HIPCHK(hipEventCreateWithFlags(&d.ev_done, hipEventDisableTiming));
-    // hist bins and list counters in one block: one memset and one copy per field.
-    HIPCHK(hipMalloc(&d.d_hist, kStateBytes));
-    d.d_count = (uint32_t *)(d.d_hist + kHistCopies * 129);
-    HIPCHK(hipHostMalloc(&d.h_hist, kStateBytes, hipHostMallocDefault));
-    d.h_count = (uint32_t *)(d.h_hist + kHistCopies * 129);
-    HIPCHK(hipHostMalloc(&d.h_fin, 130 * 8, hipHostMallocMapped | hipHostMallocCoherent));
-    HIPCHK(hipHostGetDevicePointer((void **)&d.d_fin, d.h_fin, 0));
-    int rc = ensure_list(d, kInitialListCap);
-    if (rc) return rc;
+    for (auto &sl : d.slot) {
+        int rc = slot_init(d, sl);
+        if (rc) return rc;
+    }
     return NICE_OK;
 }
 
 void device_free(Device &d) {
-    if (!d.stream) return;
+    if (!d.slot[0].stream) return;
     (void)hipSetDevice(d.id);
-    (void)hipStreamSynchronize(d.stream);
+    if (d.aux) (void)hipStreamSynchronize(d.aux);
+    for (auto &sl : d.slot) {
+        if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+        if (sl.nstream) (void)hipStreamSynchronize(sl.nstream);
+    }
     for (auto &kv : d.residues) (void)hipFree(kv.second);
     for (auto &kv : d.ranks) (void)hipFree(kv.second);
     for (auto &b : d.desc) {
@@ -204,27 +307,30 @@ void device_free(Device &d) {
         }
         if (b.done) (void)hipEventDestroy(b.done);
     }
-    for (auto &q : d.msd.q)
-        if (q) (void)hipFree(q);
-    if (d.msd.leaves) (void)hipFree(d.msd.leaves);
-    if (d.msd.counters) (void)hipFree(d.msd.counters);
-    if (d.msd.h_counters) (void)hipHostFree(d.msd.h_counters);
-    (void)hipFree(d.d_hist);
-    (void)hipFree(d.d_list_n);
-    (void)hipFree(d.d_list_u);
-    (void)hipHostFree(d.h_hist);
-    (void)hipHostFree(d.h_fin);
-    (void)hipEventDestroy(d.ev0);
-    (void)hipEventDestroy(d.ev1);
-    (void)hipEventDestroy(d.ev_done);
-    (void)hipStreamDestroy(d.stream);
-    d.stream = nullptr;
+    for (auto &sl : d.slot) {
+        for (auto &q : sl.msd.q)
+            if (q) (void)hipFree(q);
+        if (sl.msd.leaves) (void)hipFree(sl.msd.leaves);
+        if (sl.msd.counters) (void)hipFree(sl.msd.counters);
+        if (sl.msd.scratch) (void)hipFree(sl.msd.scratch);
+        if (sl.stream) (void)hipStreamDestroy(sl.stream);
+        if (sl.nstream) (void)hipStreamDestroy(sl.nstream);
+        if (sl.d_nice_count) (void)hipFree(sl.d_nice_count);
+        if (sl.d_nice_done) (void)hipFree(sl.d_nice_done);
+        if (sl.d_state) (void)hipFree(sl.d_state);
+        for (ListBuf *l : {&sl.det, &sl.nice}) {
+            if (l->n) (void)hipFree(l->n);
+            if (l->u) (void)hipFree(l->u);
+        }
+        if (sl.h_fin) (void)hipHostFree(sl.h_fin);
+        if (sl.h_msd) (void)hipHostFree(sl.h_msd);
+        if (sl.h_nice) (void)hipHostFree(sl.h_nice);
+        for (hipEvent_t ev : {sl.ev0, sl.ev1, sl.ev_done, sl.nice_done})
+            if (ev) (void)hipEventDestroy(ev);
+    }
+    if (d.aux) (void)hipStreamDestroy(d.aux);
+    for (auto &sl : d.slot) sl.stream = nullptr;
 }
-
-struct Entry {
-    u128 n;
-    uint32_t u;
-};
 
 int emit_list(std::vector<Entry> &all, nice_number *out, size_t cap, size_t *n_out) {
     std::sort(all.begin(), all.end(), [](const Entry &a, const Entry &b) { return a.n < b.n; });
@@ -285,12 +391,18 @@ int fd_variant() {
 #endif
 
 // Enqueue the detailed kernels for [s, e) on one device (async).
-int enqueue_detailed(Device &d, u128 s, u128 e, uint32_t base, bool &used_fd, uint64_t &fd_count) {
+// Enqueue the detailed kernels for [s, e) on one device (async): generic
+// kernel outside the base's valid range, FD kernel inside.  Returns in
+// *finished whether the last launch also finished the field (fd2's in-kernel
+// finish into the slot's mapped result words); otherwise the caller enqueues
+// the epilogue kernel.
+int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *finished) {
     nice::DetailedLaunch p{};
     p.base = base;
     p.cutoff = nice::near_miss_cutoff(base);
-    p.hist = d.d_hist;
-    p.out = nice::NumOut{d.d_list_n, d.d_list_u, d.d_count, d.list_cap};
+    p.hist = sl.d_state;
+    p.out = nice::NumOut{sl.det.n, sl.det.u, sl.d_count, sl.det.cap};
+    *finished = false;
     auto launch = [&](u128 a, u128 b, bool fd) -> int {
         if (a >= b) return NICE_OK;
         u128 cnt = b - a;
@@ -299,22 +411,23 @@ int enqueue_detailed(Device &d, u128 s, u128 e, uint32_t base, bool &used_fd, ui
             p.start_lo = lo64(a);
             p.start_hi = hi64(a);
             p.count = c;
+            // the field's last launch finishes it when it is an fd2 launch
+            const bool last = a + c == e;
+            p.fin = last && fd ? nice::FieldFinish{sl.d_fin, sl.d_done} : nice::FieldFinish{nullptr, nullptr};
 #ifdef NICE_PROBES
             const int var = fd_variant();
-            hipError_t err = !fd ? nice::launch_detailed_generic(p, d.num_cus, d.stream)
-                             : var == 0 && nice::fd2_supported(base)
-                                 ? nice::launch_detailed_fd2(p, d.num_cus, d.stream)
-                                 : nice::launch_detailed_fd(p, d.num_cus, d.stream, var);
+            const bool fd2 = fd && var == 0 && nice::fd2_supported(base);
+            hipError_t err = !fd ? nice::launch_detailed_generic(p, d.num_cus, sl.stream)
+                             : fd2 ? nice::launch_detailed_fd2(p, d.num_cus, sl.stream)
+                                   : nice::launch_detailed_fd(p, d.num_cus, sl.stream, var);
 #else
-            hipError_t err = fd ? nice::launch_detailed_fd2(p, d.num_cus, d.stream)
-                                : nice::launch_detailed_generic(p, d.num_cus, d.stream);
+            const bool fd2 = fd;
+            hipError_t err = fd ? nice::launch_detailed_fd2(p, d.num_cus, sl.stream)
+                                : nice::launch_detailed_generic(p, d.num_cus, sl.stream);
 #endif
             if (err != hipSuccess)
                 return fail(NICE_ERR_HIP, std::string("detailed launch: ") + hipGetErrorString(err));
-            if (fd) {
-                used_fd = true;
-                fd_count += c;
-            }
+            if (last) *finished = fd2;
             a += c;
             cnt -= c;
         }
@@ -332,6 +445,153 @@ int enqueue_detailed(Device &d, u128 s, u128 e, uint32_t base, bool &used_fd, ui
     if ((rc = launch(s, std::min(e, rs), false))) return rc;
     if ((rc = launch(std::max(s, rs), std::min(e, re), true))) return rc;
     return launch(std::max(s, re), e, false);
+}
+
+// Enqueue one device's shard of a detailed field into slot `sl` (async).
+int enqueue_detailed_shard(Device &d, Slot &sl, u128 s, u128 e, uint32_t base) {
+    HIPCHK(hipSetDevice(d.id));
+    // The state block is zeroed by the previous field's finish; a memset
+    // only after an interrupted field (or the first one).
+    if (sl.dirty) HIPCHK(hipMemsetAsync(sl.d_state, 0, kStateBytes, sl.stream));
+    sl.dirty = true;
+    HIPCHK(hipEventRecord(sl.ev0, sl.stream));
+    bool finished = false;
+    int rc = enqueue_detailed(d, sl, s, e, base, &finished);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(sl.ev1, sl.stream));
+    if (!finished) HIPCHK(nice::launch_detailed_finish(sl.d_state, sl.d_count, sl.d_fin, sl.stream));
+    HIPCHK(hipEventRecord(sl.ev_done, sl.stream));
+    return NICE_OK;
+}
+
+int detailed_submit(nice_ctx *ctx, u128 s, u128 e, uint32_t base, int *ticket) {
+    const int t = ctx->det_next;
+    DetJob &job = ctx->det[t];
+    if (job.active)
+        return fail(NICE_ERR_INVALID, "three detailed fields already in flight on this context; collect one first");
+    const size_t nd = ctx->devs.size();
+    const u128 size = e - s;
+    // Shard bounds: contiguous, in device order (ascending n).
+    job.bounds.assign(nd + 1, 0);
+    for (size_t i = 0; i <= nd; i++) job.bounds[i] = s + size / nd * i + std::min<u128>(i, size % nd);
+    for (size_t i = 0; i < nd; i++) {
+        if (job.bounds[i] >= job.bounds[i + 1]) continue;
+        int rc = enqueue_detailed_shard(ctx->devs[i], ctx->devs[i].slot[t], job.bounds[i], job.bounds[i + 1], base);
+        if (rc) return rc;
+    }
+    job.active = true;
+    job.collected = false;
+    job.s = s;
+    job.e = e;
+    job.base = base;
+    ctx->det_next = (t + 1) % slots_used();
+    *ticket = t;
+    return NICE_OK;
+}
+
+// Wait for a submitted detailed field, merge the devices' results into the
+// job and self-check them (the server's submit invariants).
+int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
+    const uint32_t base = job.base;
+    const size_t nd = ctx->devs.size();
+    job.total.assign(base + 1, 0);
+    job.all.clear();
+    for (size_t i = 0; i < nd; i++) {
+        Device &d = ctx->devs[i];
+        Slot &sl = d.slot[t];
+        d.last = nice_kernel_stats{};
+        if (job.bounds[i] >= job.bounds[i + 1]) continue;
+        HIPCHK(hipSetDevice(d.id));
+        HIPCHK(hipEventSynchronize(sl.ev_done));
+        sl.dirty = false;  // the epilogue zeroed the state block
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, sl.ev0, sl.ev1));
+        d.last.kernel_ms = ms;
+        d.last.numbers = (uint64_t)(job.bounds[i + 1] - job.bounds[i]);
+        d.last.launches = 1;
+        d.last.fd_kernel = nice::fd2_supported(base) ? 1u : 0u;
+        uint32_t cnt = (uint32_t)sl.h_fin[129];
+        if (cnt > sl.det.cap) {
+            // Near-miss list overflowed (e.g. out-of-range n, SURVEY hazard 9):
+            // grow to the exact count and redo this shard (behind any field
+            // queued after it; only this slot's completion is awaited).
+            int rc = ensure_listbuf(d, sl.det, cnt, true);
+            if (!rc) rc = enqueue_detailed_shard(d, sl, job.bounds[i], job.bounds[i + 1], base);
+            if (rc) return rc;
+            HIPCHK(hipEventSynchronize(sl.ev_done));
+            sl.dirty = false;
+            cnt = (uint32_t)sl.h_fin[129];
+            if (cnt > sl.det.cap) return fail(NICE_ERR_HIP, "near-miss list overflow after resize");
+        }
+        for (uint32_t b = 0; b <= base; b++) job.total[b] += sl.h_fin[b];
+        if (cnt) {
+            std::vector<uint64_t> nbuf((size_t)cnt * 2);
+            std::vector<uint32_t> ubuf(cnt);
+            HIPCHK(hipMemcpy(nbuf.data(), sl.det.n, (size_t)cnt * 16, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(ubuf.data(), sl.det.u, (size_t)cnt * 4, hipMemcpyDeviceToHost));
+            for (uint32_t q = 0; q < cnt; q++) job.all.push_back({mk(nbuf[2 * q], nbuf[2 * q + 1]), ubuf[q]});
+        }
+    }
+    // Self-check: the server's submit invariants (api/src/main.rs:309-359)
+    // before anything is returned.
+    int rc = validate_detailed(base, job.e - job.s, job.total.data(), job.all.size(),
+                               [&](size_t i) { return job.all[i]; });
+    if (rc) return rc;
+    if (!job.all.empty()) {
+        // ... and its last one: every listed number's unique count recomputed
+        // by the generic per-n device function (full square / cube + digit
+        // scan, a different code path from the FD kernel that listed it), on
+        // the auxiliary stream so no queued field is waited for.
+        Device &d = ctx->devs[0];
+        HIPCHK(hipSetDevice(d.id));
+        // created on first use: an idle stream would still take one of the
+        // process's few hardware queues (GPU_MAX_HW_QUEUES)
+        if (!d.aux) HIPCHK(hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking));
+        const size_t n = job.all.size();
+        std::vector<uint64_t> pairs(2 * n);
+        for (size_t i = 0; i < n; i++) {
+            pairs[2 * i] = lo64(job.all[i].n);
+            pairs[2 * i + 1] = hi64(job.all[i].n);
+        }
+        uint64_t *dn = nullptr;
+        uint32_t *du = nullptr;
+        HIPCHK(hipMalloc(&dn, n * 16));
+        HIPCHK(hipMalloc(&du, n * 4));
+        std::vector<uint32_t> u(n);
+        hipError_t err = hipMemcpyAsync(dn, pairs.data(), n * 16, hipMemcpyHostToDevice, d.aux);
+        if (err == hipSuccess) err = nice::launch_unique_counts(dn, (uint32_t)n, base, du, d.aux);
+        if (err == hipSuccess) err = hipMemcpyAsync(u.data(), du, n * 4, hipMemcpyDeviceToHost, d.aux);
+        if (err == hipSuccess) err = hipStreamSynchronize(d.aux);
+        (void)hipFree(dn);
+        (void)hipFree(du);
+        if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("self-check: ") + hipGetErrorString(err));
+        for (size_t i = 0; i < n; i++)
+            if (u[i] != job.all[i].u)
+                return fail(NICE_ERR_HIP, "self-check: unique count of a listed number does not recompute");
+    }
+    std::sort(job.all.begin(), job.all.end(), [](const Entry &a, const Entry &b) { return a.n < b.n; });
+    return NICE_OK;
+}
+
+int detailed_collect(nice_ctx *ctx, int t, uint64_t *hist, nice_number *out, size_t cap, size_t *n_out) {
+    if (t < 0 || t >= kSlots || !ctx->det[t].active)
+        return fail(NICE_ERR_INVALID, "no detailed field in flight under this ticket");
+    DetJob &job = ctx->det[t];
+    if (!job.collected) {
+        int rc = detailed_gather(ctx, job, t);
+        if (rc) {
+            job.active = false;  // the field is lost; its slot is reusable
+            for (auto &d : ctx->devs) d.slot[t].dirty = true;
+            return rc;
+        }
+        job.collected = true;
+    }
+    std::memcpy(hist, job.total.data(), (job.base + 1) * 8);
+    int rc = emit_list(job.all, out, cap, n_out);
+    if (rc == NICE_ERR_CAPACITY) return rc;  // kept: the caller retries with room
+    job.active = false;
+    job.all = {};
+    return rc;
 }
 
 }  // namespace
@@ -404,109 +664,35 @@ int nice_last_kernel_stats(nice_ctx *ctx, int i, nice_kernel_stats *out) {
 int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi,
                                 uint64_t end_lo, uint64_t end_hi, uint32_t base, uint64_t *hist,
                                 nice_number *out, size_t cap, size_t *n_out) {
-    if (!ctx || !hist) return fail(NICE_ERR_INVALID, "null argument");
+    int t = -1;
+    int rc = nice_detailed_submit(ctx, start_lo, start_hi, end_lo, end_hi, base, &t);
+    if (rc) return rc;
+    rc = nice_detailed_collect(ctx, t, hist, out, cap, n_out);
+    if (rc == NICE_ERR_CAPACITY) {
+        // synchronous call: the caller retries the whole field with room
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        ctx->det[t].active = false;
+        ctx->det[t].all = {};
+    }
+    return rc;
+}
+
+int nice_detailed_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, uint64_t end_lo,
+                         uint64_t end_hi, uint32_t base, int *ticket) {
+    if (!ctx || !ticket) return fail(NICE_ERR_INVALID, "null argument");
     if (base < 2 || base > 128) return fail(NICE_ERR_INVALID, "base must be in 2..=128");
     const u128 s = mk(start_lo, start_hi), e = mk(end_lo, end_hi);
     if (s >= e)
         return fail(NICE_ERR_INVALID, "Range has invalid bounds, range_start must be < range_end");
     std::lock_guard<std::mutex> lock(ctx->mu);
-    const size_t nd = ctx->devs.size();
-    const u128 size = e - s;
-    // Shard bounds: contiguous, in device order (ascending n).
-    std::vector<u128> bounds(nd + 1);
-    for (size_t i = 0; i <= nd; i++) bounds[i] = s + size / nd * i + std::min<u128>(i, size % nd);
-    for (size_t i = 0; i < nd; i++) {
-        Device &d = ctx->devs[i];
-        d.last = nice_kernel_stats{};
-        if (bounds[i] >= bounds[i + 1]) continue;
-        HIPCHK(hipSetDevice(d.id));
-        // The state block is zeroed by the previous field's epilogue; a
-        // memset only after an interrupted field (or the first one).
-        if (d.state_dirty) HIPCHK(hipMemsetAsync(d.d_hist, 0, kStateBytes, d.stream));
-        d.state_dirty = true;
-        HIPCHK(hipEventRecord(d.ev0, d.stream));
-        bool used_fd = false;
-        uint64_t fdc = 0;
-        int rc = enqueue_detailed(d, bounds[i], bounds[i + 1], base, used_fd, fdc);
-        if (rc) return rc;
-        HIPCHK(hipEventRecord(d.ev1, d.stream));
-        HIPCHK(nice::launch_detailed_finish(d.d_hist, d.d_count, d.d_fin, d.stream));
-        HIPCHK(hipEventRecord(d.ev_done, d.stream));
-        d.last.fd_kernel = used_fd;
-        d.last.numbers = (uint64_t)(bounds[i + 1] - bounds[i]);
-        d.last.launches = 1;
-    }
-    std::vector<uint64_t> total(base + 1, 0);
-    std::vector<Entry> all;
-    for (size_t i = 0; i < nd; i++) {
-        Device &d = ctx->devs[i];
-        if (bounds[i] >= bounds[i + 1]) continue;
-        HIPCHK(hipSetDevice(d.id));
-        HIPCHK(hipEventSynchronize(d.ev_done));
-        d.state_dirty = false;  // the epilogue zeroed the state block
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, d.ev0, d.ev1));
-        d.last.kernel_ms = ms;
-        uint32_t cnt = (uint32_t)d.h_fin[129];
-        if (cnt > d.list_cap) {
-            // Near-miss list overflowed (e.g. out-of-range n, SURVEY hazard 9):
-            // grow to the exact count and redo this shard.
-            int rc = ensure_list(d, cnt);
-            if (rc) return rc;
-            d.state_dirty = true;
-            bool used_fd = false;
-            uint64_t fdc = 0;
-            rc = enqueue_detailed(d, bounds[i], bounds[i + 1], base, used_fd, fdc);
-            if (rc) return rc;
-            HIPCHK(nice::launch_detailed_finish(d.d_hist, d.d_count, d.d_fin, d.stream));
-            HIPCHK(hipStreamSynchronize(d.stream));
-            d.state_dirty = false;
-            cnt = (uint32_t)d.h_fin[129];
-            if (cnt > d.list_cap) return fail(NICE_ERR_HIP, "near-miss list overflow after resize");
-        }
-        for (uint32_t b = 0; b <= base; b++) total[b] += d.h_fin[b];
-        if (cnt) {
-            std::vector<uint64_t> nbuf((size_t)cnt * 2);
-            std::vector<uint32_t> ubuf(cnt);
-            HIPCHK(hipMemcpy(nbuf.data(), d.d_list_n, (size_t)cnt * 16, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(ubuf.data(), d.d_list_u, (size_t)cnt * 4, hipMemcpyDeviceToHost));
-            for (uint32_t q = 0; q < cnt; q++) all.push_back({mk(nbuf[2 * q], nbuf[2 * q + 1]), ubuf[q]});
-        }
-    }
-    std::memcpy(hist, total.data(), (base + 1) * 8);
-    // Self-check: the server's submit invariants (api/src/main.rs:309-359)
-    // before anything is returned.
-    int rc = validate_detailed(base, size, total.data(), all.size(), [&](size_t i) { return all[i]; });
-    if (rc) return rc;
-    if (!all.empty()) {
-        // ... and its last one: every listed number's unique count recomputed
-        // by the generic per-n device function (full square / cube + digit
-        // scan, a different code path from the FD kernel that listed it).
-        Device &d = ctx->devs[0];
-        HIPCHK(hipSetDevice(d.id));
-        const size_t n = all.size();
-        std::vector<uint64_t> pairs(2 * n);
-        for (size_t i = 0; i < n; i++) {
-            pairs[2 * i] = lo64(all[i].n);
-            pairs[2 * i + 1] = hi64(all[i].n);
-        }
-        uint64_t *dn = nullptr;
-        uint32_t *du = nullptr;
-        HIPCHK(hipMalloc(&dn, n * 16));
-        HIPCHK(hipMalloc(&du, n * 4));
-        std::vector<uint32_t> u(n);
-        hipError_t err = hipMemcpyAsync(dn, pairs.data(), n * 16, hipMemcpyHostToDevice, d.stream);
-        if (err == hipSuccess) err = nice::launch_unique_counts(dn, (uint32_t)n, base, du, d.stream);
-        if (err == hipSuccess) err = hipMemcpyAsync(u.data(), du, n * 4, hipMemcpyDeviceToHost, d.stream);
-        if (err == hipSuccess) err = hipStreamSynchronize(d.stream);
-        (void)hipFree(dn);
-        (void)hipFree(du);
-        if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("self-check: ") + hipGetErrorString(err));
-        for (size_t i = 0; i < n; i++)
-            if (u[i] != all[i].u)
-                return fail(NICE_ERR_HIP, "self-check: unique count of a listed number does not recompute");
-    }
-    return emit_list(all, out, cap, n_out);
+    return detailed_submit(ctx, s, e, base, ticket);
+}
+
+int nice_detailed_collect(nice_ctx *ctx, int ticket, uint64_t *hist, nice_number *out, size_t cap,
+                          size_t *n_out) {
+    if (!ctx || !hist) return fail(NICE_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    return detailed_collect(ctx, ticket, hist, out, cap, n_out);
 }
 
 int nice_validate_detailed(uint32_t base, uint64_t size_lo, uint64_t size_hi, const uint64_t *hist,
@@ -529,8 +715,8 @@ int nice_debug_unique_counts(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t co
     HIPCHK(hipMalloc(&dn, (size_t)count * 16));
     HIPCHK(hipMalloc(&du, (size_t)count * 4));
     HIPCHK(hipMemcpy(dn, n_pairs, (size_t)count * 16, hipMemcpyHostToDevice));
-    HIPCHK(nice::launch_unique_counts(dn, count, base, du, d.stream));
-    HIPCHK(hipStreamSynchronize(d.stream));
+    HIPCHK(nice::launch_unique_counts(dn, count, base, du, d.slot[0].stream));
+    HIPCHK(hipStreamSynchronize(d.slot[0].stream));
     HIPCHK(hipMemcpy(out, du, (size_t)count * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipFree(dn));
     HIPCHK(hipFree(du));
@@ -548,8 +734,8 @@ int nice_debug_is_nice(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t count, u
     HIPCHK(hipMalloc(&dn, (size_t)count * 16));
     HIPCHK(hipMalloc(&du, (size_t)count * 4));
     HIPCHK(hipMemcpy(dn, n_pairs, (size_t)count * 16, hipMemcpyHostToDevice));
-    HIPCHK(nice::launch_is_nice(dn, count, base, du, d.stream));
-    HIPCHK(hipStreamSynchronize(d.stream));
+    HIPCHK(nice::launch_is_nice(dn, count, base, du, d.slot[0].stream));
+    HIPCHK(hipStreamSynchronize(d.slot[0].stream));
     HIPCHK(hipMemcpy(out, du, (size_t)count * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipFree(dn));
     HIPCHK(hipFree(du));
@@ -634,6 +820,10 @@ int nice_stride_table(uint32_t base, uint32_t k, uint64_t *modulus, uint32_t *re
 // NICE_GPU_MSD_FLOOR pins the reference GPU path's MSD floor
 // (client_process_gpu.rs:161-172: parsed as f64, used when >= 1, otherwise
 // ignored with a warning).  Read once, like the reference's OnceLock.
+static uint64_t nbatches_of(uint64_t chunks, uint64_t per_batch) {
+    return (chunks + per_batch - 1) / per_batch;
+}
+
 static uint64_t env_msd_floor() {
     static const uint64_t v = [] {
         const char *e = getenv("NICE_GPU_MSD_FLOOR");
@@ -649,13 +839,11 @@ static uint64_t env_msd_floor() {
     return v;
 }
 
-int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi,
-                                   uint64_t end_lo, uint64_t end_hi, uint32_t base,
-                                   const nice_niceonly_opts *opts, nice_number *out, size_t cap,
-                                   size_t *n_out, nice_niceonly_stats *stats) {
+int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, uint64_t end_lo,
+                         uint64_t end_hi, uint32_t base, const nice_niceonly_opts *opts, int *ticket) {
     using clock = std::chrono::steady_clock;
     const auto t0 = clock::now();
-    if (!ctx) return fail(NICE_ERR_INVALID, "null ctx");
+    if (!ctx || !ticket) return fail(NICE_ERR_INVALID, "null argument");
     if (base < 3 || base > 128) return fail(NICE_ERR_INVALID, "base must be in 3..=128");
     const u128 s = mk(start_lo, start_hi), e = mk(end_lo, end_hi);
     if (s >= e)
@@ -682,10 +870,23 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
     };
 
     std::lock_guard<std::mutex> lock(ctx->mu);
-    if (nice::residue_filter(base).empty() || mine == 0) {  // client_process_gpu.rs:525-531
-        if (stats) *stats = st;
-        if (n_out) *n_out = 0;
+    const int t = ctx->nice_next;
+    NiceJob &job = ctx->nice[t];
+    if (job.active)
+        return fail(NICE_ERR_INVALID, "three niceonly fields already in flight on this context; collect one first");
+    job = NiceJob{};
+    job.base = base;
+    job.t0 = t0;
+    job.used.assign(ctx->devs.size(), 0);
+    auto finish_submit = [&]() {
+        job.active = true;
+        ctx->nice_next = (t + 1) % slots_used();
+        *ticket = t;
         return NICE_OK;
+    };
+    if (nice::residue_filter(base).empty() || mine == 0) {  // client_process_gpu.rs:525-531
+        job.empty = true;
+        return finish_submit();
     }
     auto table = g_stride.get(base, k);
     // Whole field inside the base's valid range: the kernels take their
@@ -714,9 +915,6 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
             HIPCHK(hipMemcpy(p, rank.data(), rank.size() * 4, hipMemcpyHostToDevice));
             d.ranks[base * 8 + k] = p;
         }
-        HIPCHK(hipMemsetAsync(d.d_count + 1, 0, 4, d.stream));
-        int rc = ensure_list(d, kNiceCap);
-        if (rc) return rc;
     }
 
     // Device MSD: batches of this caller's chunks, each run as init + the
@@ -736,19 +934,34 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
         per = std::min<uint64_t>(per, 1ull << 26);
         // leaf records: one per range plus one per kLeafPiece candidates
         const uint64_t leaf_cap = std::min<uint64_t>(per + (batch_n / nice::kLeafPiece) + 64, 0xffffffffull);
-        for (auto &d : ctx->devs) {
+        // Chunks whose recursion fits a workgroup run fused: one launch per
+        // batch, one workgroup per chunk (grid-strided), no level queues.
+        const uint32_t fcap = nice::msd_fused_cap(cnk, floor_size);
+        const uint64_t nbatches = nbatches_of(mine, cpb);
+        for (size_t i = 0; i < ctx->devs.size(); i++) {
+            Device &d = ctx->devs[i];
             HIPCHK(hipSetDevice(d.id));
-            int r = ensure_msd(d, (uint32_t)per, (uint32_t)leaf_cap);
+            const uint64_t fgrid = std::min<uint64_t>(cpb, (uint64_t)d.num_cus * 4);
+            int r = fcap ? ensure_msd(d.slot[t], 0, (uint32_t)leaf_cap, fgrid * 2 * fcap)
+                         : ensure_msd(d.slot[t], (uint32_t)per, (uint32_t)leaf_cap, 0);
             if (r) return r;
-            HIPCHK(hipMemsetAsync(d.msd.counters, 0, 32 * 4, d.stream));
+            if (i < nbatches) {
+                job.used[i] = 1;
+                if (d.slot[t].msd.dirty) {  // first use / after an interrupted field
+                    HIPCHK(hipMemsetAsync(d.slot[t].msd.counters, 0, 32 * 4, d.slot[t].nstream));
+                    HIPCHK(hipMemsetAsync(d.slot[t].d_nice_count, 0, 4, d.slot[t].nstream));
+                }
+                d.slot[t].msd.dirty = true;  // until this field's epilogue is seen
+            }
         }
-        const uint64_t nbatches = (mine + cpb - 1) / cpb;
         for (uint64_t bi = 0; bi < nbatches; bi++) {
             Device &d = ctx->devs[bi % ctx->devs.size()];
             HIPCHK(hipSetDevice(d.id));
-            if (bi >= ctx->devs.size())  // first batch per device: zeroed above
-                HIPCHK(hipMemsetAsync(d.msd.counters, 0, 25 * 4, d.stream));
+            const bool first = bi < ctx->devs.size();  // this device's first batch of the field
+            const bool last = bi + ctx->devs.size() >= nbatches;  // ... and its last
             nice::MsdLaunch mp{};
+            mp.first_batch = first ? 1u : 0u;
+            mp.nice_count = d.slot[t].d_nice_count;
             mp.start_lo = lo64(s);
             mp.start_hi = hi64(s);
             mp.end_lo = lo64(e);
@@ -759,12 +972,13 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
             mp.deal_offset = deal_offset;
             mp.chunk = cnk;
             mp.floor_size = floor_size;
-            mp.q[0] = d.msd.q[0];
-            mp.q[1] = d.msd.q[1];
-            mp.counters = d.msd.counters;
-            mp.q_cap = d.msd.q_cap;
-            mp.leaves = d.msd.leaves;
-            mp.leaf_cap = d.msd.leaf_cap;
+            const MsdBuf &mb = d.slot[t].msd;
+            mp.q[0] = mb.q[0];
+            mp.q[1] = mb.q[1];
+            mp.counters = mb.counters;
+            mp.q_cap = mb.q_cap;
+            mp.leaves = mb.leaves;
+            mp.leaf_cap = mb.leaf_cap;
             mp.residues = d.residues[base * 8 + k];
             mp.ranks = d.ranks[base * 8 + k];
             mp.R = R;
@@ -774,44 +988,34 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
 #ifdef NICE_PROBES
             mp.probe = getenv("NICE_MSD_PROBE") ? (uint32_t)atoi(getenv("NICE_MSD_PROBE")) : 0u;
 #endif
-            hipError_t err = nice::launch_msd_device(mp, d.num_cus, d.stream);
+            const uint32_t fgrid = (uint32_t)std::min<uint64_t>(mp.nchunks, (uint64_t)d.num_cus * 4);
+            hipError_t err = fcap ? nice::launch_msd_device(mp, d.num_cus, d.slot[t].nstream, mb.scratch, fcap, fgrid)
+                                  : nice::launch_msd_device(mp, d.num_cus, d.slot[t].nstream);
             if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("msd launch: ") + hipGetErrorString(err));
             nice::NiceonlyLaunch p{};
-            p.leaves = d.msd.leaves;
-            p.n_leaves_dev = d.msd.counters + 24;
-            p.n_leaves = d.msd.leaf_cap;  // clamp for the device count
+            p.leaves = mb.leaves;
+            p.n_leaves_dev = mb.counters + 24;
+            p.n_leaves = mb.leaf_cap;  // clamp for the device count
             p.residues = mp.residues;
             p.R = R;
             p.M = (uint32_t)M;
             p.base = base;
             p.in_range = in_range;
-            p.out = nice::NumOut{d.d_list_n, nullptr, d.d_count + 1, d.list_cap};
-            err = nice::launch_niceonly(p, d.num_cus, d.stream);
+            p.out = nice::NumOut{d.slot[t].nice.n, nullptr, d.slot[t].d_nice_count, d.slot[t].nice.cap};
+            // epilogue: re-zero the batch's leaf count; at the field's end the
+            // results land in mapped memory (no copy launches)
+            p.fin = last ? nice::NiceFinish{d.slot[t].d_msd_mapped, d.slot[t].d_nice_mapped, mb.counters,
+                                            d.slot[t].d_nice_done}
+                         : nice::NiceFinish{nullptr, nullptr, mb.counters, d.slot[t].d_nice_done};
+            err = nice::launch_niceonly(p, d.num_cus, d.slot[t].nstream);
             if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("niceonly launch: ") + hipGetErrorString(err));
             st.launches++;
         }
-        for (auto &d : ctx->devs) {
+        for (size_t i = 0; i < ctx->devs.size(); i++) {
+            if (!job.used[i]) continue;
+            Device &d = ctx->devs[i];
             HIPCHK(hipSetDevice(d.id));
-            HIPCHK(hipMemcpyAsync(d.msd.h_counters, d.msd.counters, 32 * 4, hipMemcpyDeviceToHost,
-                                  d.stream));
-            HIPCHK(hipStreamSynchronize(d.stream));
-            const uint32_t *c = d.msd.h_counters;
-#ifdef NICE_PROBES
-            if (getenv("NICE_MSD_TRACE")) {  // level sizes of the last batch (diagnostics)
-                fprintf(stderr, "msd levels:");
-                for (int lv = 0; lv < 24; lv++) fprintf(stderr, " %u", c[lv]);
-                fprintf(stderr, " | ranges %u\n", c[26]);
-            }
-#endif
-            if (c[25])
-                return fail(NICE_ERR_CAPACITY, "device MSD queue overflow (msd_floor too small for "
-                                               "chunk_size); use msd_where = host");
-            uint64_t cand, nums;
-            std::memcpy(&cand, c + 28, 8);
-            std::memcpy(&nums, c + 30, 8);
-            st.ranges += c[26];
-            st.candidates += cand;
-            st.range_numbers += nums;
+            HIPCHK(hipEventRecord(d.slot[t].nice_done, d.slot[t].nstream));
         }
         return NICE_OK;
     };
@@ -820,10 +1024,16 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
     if (where < NICE_MSD_AUTO || where > NICE_MSD_DEVICE) return fail(NICE_ERR_INVALID, "bad msd_where");
     const bool on_device = where == NICE_MSD_DEVICE ||
                            (where == NICE_MSD_AUTO && k == 2 && !((e - s) >> 63) && chunk <= ((u128)1 << 40));
+    job.on_device = on_device;
     int rc = NICE_OK;
     if (on_device) {
         rc = run_device();
     } else {
+        for (auto &d : ctx->devs) {
+            HIPCHK(hipSetDevice(d.id));
+            HIPCHK(hipMemsetAsync(d.slot[t].d_nice_count, 0, 4, d.slot[t].nstream));
+            d.slot[t].msd.dirty = true;  // the nice count is left set
+        }
         // Producer: worker threads run the MSD filter per chunk and hand the
         // surviving ranges to this thread in chunk batches.
         std::atomic<uint64_t> next{0};
@@ -862,7 +1072,9 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
         std::vector<std::pair<u128, u128>> pend;
         auto flush = [&]() -> int {
             if (pend.empty()) return NICE_OK;
-            Device &d = ctx->devs[dev_rr++ % ctx->devs.size()];
+            const size_t di = dev_rr++ % ctx->devs.size();
+            Device &d = ctx->devs[di];
+            job.used[di] = 1;
             HIPCHK(hipSetDevice(d.id));
             LeafBuf &b = d.desc[d.desc_next];
             d.desc_next ^= 1;
@@ -896,7 +1108,7 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
             if (!nr) return NICE_OK;
             st.candidates += total;
             HIPCHK(hipMemcpyAsync(b.d, b.h, (size_t)nr * sizeof(nice::Leaf), hipMemcpyHostToDevice,
-                                  d.stream));
+                                  d.slot[t].nstream));
             nice::NiceonlyLaunch p{};
             p.leaves = b.d;
             p.n_leaves_dev = nullptr;
@@ -906,10 +1118,10 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
             p.M = (uint32_t)M;
             p.base = base;
             p.in_range = in_range;
-            p.out = nice::NumOut{d.d_list_n, nullptr, d.d_count + 1, d.list_cap};
-            hipError_t err = nice::launch_niceonly(p, d.num_cus, d.stream);
+            p.out = nice::NumOut{d.slot[t].nice.n, nullptr, d.slot[t].d_nice_count, d.slot[t].nice.cap};
+            hipError_t err = nice::launch_niceonly(p, d.num_cus, d.slot[t].nstream);
             if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("niceonly launch: ") + hipGetErrorString(err));
-            HIPCHK(hipEventRecord(b.done, d.stream));
+            HIPCHK(hipEventRecord(b.done, d.slot[t].nstream));
             b.pending = true;
             st.launches++;
             return NICE_OK;
@@ -930,28 +1142,100 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
         for (auto &w : workers) w.join();
         st.msd_seconds = std::chrono::duration<double>(clock::now() - t0).count();
         if (!rc) rc = flush();
-    }
-    if (rc) return rc;
-
-    std::vector<Entry> all;
-    for (auto &d : ctx->devs) {
-        HIPCHK(hipSetDevice(d.id));
-        HIPCHK(hipMemcpyAsync(d.h_count + 1, d.d_count + 1, 4, hipMemcpyDeviceToHost, d.stream));
-        HIPCHK(hipStreamSynchronize(d.stream));
-        for (auto &b : d.desc) b.pending = false;
-        uint32_t cnt = d.h_count[1];
-        if (cnt > d.list_cap)
-            return fail(NICE_ERR_HIP, "niceonly output buffer overflow: " + std::to_string(cnt) +
-                                          " (this strongly suggests a kernel bug)");
-        if (cnt) {
-            std::vector<uint64_t> nbuf((size_t)cnt * 2);
-            HIPCHK(hipMemcpy(nbuf.data(), d.d_list_n, (size_t)cnt * 16, hipMemcpyDeviceToHost));
-            for (uint32_t q = 0; q < cnt; q++) all.push_back({mk(nbuf[2 * q], nbuf[2 * q + 1]), base});
+        // End of the field on every device: its list count, then a marker.
+        for (size_t i = 0; i < ctx->devs.size() && !rc; i++) {
+            Device &d = ctx->devs[i];
+            job.used[i] = 1;
+            HIPCHK(hipSetDevice(d.id));
+            HIPCHK(hipMemcpyAsync(d.slot[t].h_nice, d.slot[t].d_nice_count, 4, hipMemcpyDeviceToHost,
+                                  d.slot[t].nstream));
+            HIPCHK(hipEventRecord(d.slot[t].nice_done, d.slot[t].nstream));
         }
     }
-    st.total_seconds = std::chrono::duration<double>(clock::now() - t0).count();
-    if (stats) *stats = st;
-    return emit_list(all, out, cap, n_out);
+    if (rc) return rc;
+    job.st = st;
+    return finish_submit();
+}
+
+int nice_niceonly_collect(nice_ctx *ctx, int t, nice_number *out, size_t cap, size_t *n_out,
+                          nice_niceonly_stats *stats) {
+    if (!ctx) return fail(NICE_ERR_INVALID, "null ctx");
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    if (t < 0 || t >= kSlots || !ctx->nice[t].active)
+        return fail(NICE_ERR_INVALID, "no niceonly field in flight under this ticket");
+    NiceJob &job = ctx->nice[t];
+    if (!job.collected) {
+        auto gather = [&]() -> int {
+            for (size_t i = 0; i < ctx->devs.size(); i++) {
+                Device &d = ctx->devs[i];
+                Slot &sl = d.slot[t];
+                if (!job.used[i]) continue;  // no batch of this field ran there
+                HIPCHK(hipSetDevice(d.id));
+                HIPCHK(hipEventSynchronize(sl.nice_done));
+                if (job.on_device && job.used[i]) {
+                    const uint32_t *c = sl.h_msd;
+                    sl.msd.dirty = false;  // the epilogue re-zeroed counters and count
+#ifdef NICE_PROBES
+                    if (getenv("NICE_MSD_TRACE")) {  // level sizes of the last batch (diagnostics)
+                        fprintf(stderr, "msd levels:");
+                        for (int lv = 0; lv < 24; lv++) fprintf(stderr, " %u", c[lv]);
+                        fprintf(stderr, " | ranges %u\n", c[26]);
+                    }
+#endif
+                    if (c[25])
+                        return fail(NICE_ERR_CAPACITY, "device MSD queue overflow (msd_floor too small "
+                                                       "for chunk_size); use msd_where = host");
+                    uint64_t cand, nums;
+                    std::memcpy(&cand, c + 28, 8);
+                    std::memcpy(&nums, c + 30, 8);
+                    job.st.ranges += c[26];
+                    job.st.candidates += cand;
+                    job.st.range_numbers += nums;
+                }
+                const uint32_t cnt = *sl.h_nice;
+                if (cnt > sl.nice.cap)
+                    return fail(NICE_ERR_HIP, "niceonly output buffer overflow: " + std::to_string(cnt) +
+                                                  " (this strongly suggests a kernel bug)");
+                if (cnt) {
+                    std::vector<uint64_t> nbuf((size_t)cnt * 2);
+                    HIPCHK(hipMemcpy(nbuf.data(), sl.nice.n, (size_t)cnt * 16, hipMemcpyDeviceToHost));
+                    for (uint32_t q = 0; q < cnt; q++)
+                        job.all.push_back({mk(nbuf[2 * q], nbuf[2 * q + 1]), job.base});
+                }
+            }
+            return NICE_OK;
+        };
+        const int rc = job.empty ? NICE_OK : gather();
+        if (rc) {
+            job.active = false;
+            return rc;
+        }
+        job.st.total_seconds =
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - job.t0).count();
+        job.collected = true;
+    }
+    if (stats) *stats = job.st;
+    const int rc = emit_list(job.all, out, cap, n_out);
+    if (rc == NICE_ERR_CAPACITY) return rc;  // kept: the caller retries with room
+    job.active = false;
+    job.all = {};
+    return rc;
+}
+
+int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi,
+                                   uint64_t end_lo, uint64_t end_hi, uint32_t base,
+                                   const nice_niceonly_opts *opts, nice_number *out, size_t cap,
+                                   size_t *n_out, nice_niceonly_stats *stats) {
+    int t = -1;
+    int rc = nice_niceonly_submit(ctx, start_lo, start_hi, end_lo, end_hi, base, opts, &t);
+    if (rc) return rc;
+    rc = nice_niceonly_collect(ctx, t, out, cap, n_out, stats);
+    if (rc == NICE_ERR_CAPACITY) {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        ctx->nice[t].active = false;
+        ctx->nice[t].all = {};
+    }
+    return rc;
 }
 
 int nice_process_range_niceonly(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi,

@@ -96,6 +96,36 @@ niceonly_kernel(NiceonlyLaunch p, G g) {
             }
         }
     }
+    if (p.fin.done) {
+        // last workgroup: the field's results to mapped host memory (the
+        // count is agent-atomic, so: own atomics drained, barrier, one agent
+        // add per workgroup -- no L2 write-back fence, see fd2's field_finish)
+        __shared__ u32 last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) last = atomicAdd(p.fin.done, 1u) == gridDim.x - 1;
+        __syncthreads();
+        if (last) {
+            // Field end (count_mapped set): results out, then the field's
+            // counters re-zeroed for the slot's next field.  Batch end: only
+            // the per-batch leaf-record count, for the next batch.
+            u32 *ctr = p.fin.msd_counters;
+            const u32 w = threadIdx.x;
+            if (p.fin.count_mapped) {
+                if (ctr && w < 32) {
+                    p.fin.msd_mapped[w] = __hip_atomic_load(&ctr[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (w >= 24) __hip_atomic_store(&ctr[w], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (w == 0) {
+                    *p.fin.count_mapped = __hip_atomic_load(p.out.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(p.out.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else if (ctr && w == 24) {
+                __hip_atomic_store(&ctr[24], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (w == 0) __hip_atomic_store(p.fin.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 __global__ void is_nice_kernel(const u64 *n_pairs, u32 count, GenericBase g, u32 *out) {
@@ -286,7 +316,14 @@ __global__ void msd_init_kernel(MsdLaunch p) {
         const u64 size = rem_hi || rem_lo > p.chunk ? p.chunk : rem_lo;
         p.q[0][i] = MsdNode{lo, hi, size, 0u, 0u};
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) p.counters[0] = (u32)p.nchunks;
+    // counters: [0] level-0 size, [1..24] per batch, [25..31] sticky over the
+    // field (zeroed with the first batch, as is the field's nice count)
+    if (blockIdx.x == 0 && threadIdx.x < 32) {
+        const u32 w = threadIdx.x;
+        if (w == 0) p.counters[0] = (u32)p.nchunks;
+        else if (w < 25 || p.first_batch) p.counters[w] = 0;
+        if (w == 0 && p.first_batch) *p.nice_count = 0;
+    }
 }
 
 // Reserve `mine` slots per thread of a 256-thread workgroup with ONE atomic
@@ -318,98 +355,79 @@ __device__ __forceinline__ u32 block_reserve(u32 *ctr, u32 mine, u32 *slots) {
     return base + before + incl - mine;
 }
 
-template <class G, u32 MC>
-__global__ void __launch_bounds__(256)
-msd_level_kernel(MsdLaunch p, u32 level, G g) {
-    __shared__ u32 slots[4];
-    __shared__ unsigned long long stat[3];
-    if (threadIdx.x < 3) stat[threadIdx.x] = 0;
-    const MsdNode *qin = p.q[level & 1];
-    MsdNode *qout = p.q[(level + 1) & 1];
-    const u32 n_in = p.counters[level];
-    const u32 lane = threadIdx.x & 63;
-    // Workgroup-uniform loop: leaves and children are appended with one atomic
-    // per workgroup, statistics summed in LDS and added once at the end.
-    const u32 stride = gridDim.x * blockDim.x;
-    u64 n_st = 0, c_st = 0, s_st = 0;
-    for (u32 b0 = blockIdx.x * blockDim.x; b0 < n_in; b0 += stride) {
-        const u32 i = b0 + threadIdx.x;
-        u32 act = 0;  // 0 drop / idle, 1 leaf, 2 split
-        MsdNode nd{0, 0, 0, 0, 0};
-        if (i < n_in) {
-            nd = qin[i];
-            bool leaf = level >= 22 || nd.size <= p.floor_size;
-            bool skip = false;
-            if (!leaf) {
-                u64 l_lo = nd.lo, l_hi = nd.hi;
-                add_u128(l_lo, l_hi, nd.size - 1);
+// The recursion's rule for one node (msd_prefix_filter.rs:583-658):
+// 0 = dropped (has_duplicate_msd_prefix), 1 = leaf, 2 = split in two.
+template <class G>
+__device__ __forceinline__ u32 classify_node(const MsdLaunch &p, u32 level, u64 lo, u64 hi, u64 size,
+                                             const G &g) {
+    bool leaf = level >= 22 || size <= p.floor_size;
+    if (leaf) return 1;
+    u64 l_lo = lo, l_hi = hi;
+    add_u128(l_lo, l_hi, size - 1);
 #ifdef NICE_PROBES
-                const bool no_skip_test = p.probe & 1;
+    const bool no_skip_test = p.probe & 1;
 #else
-                constexpr bool no_skip_test = false;
+    constexpr bool no_skip_test = false;
 #endif
-                if (nd.size != 1 && !no_skip_test) {
-                    if constexpr (IsConst<G>::value) {
-                        skip = p.in_range ? msd_skippable_fast<IsConst<G>::base>(nd.lo, nd.hi, l_lo, l_hi)
-                                          : msd_skippable<G>(nd.lo, nd.hi, l_lo, l_hi, g);
-                    } else {
-                        skip = msd_skippable<G>(nd.lo, nd.hi, l_lo, l_hi, g);
-                    }
-                }
-                leaf = nd.size < 2 * p.floor_size;
-            }
-            act = skip ? 0u : (leaf ? 1u : 2u);
-        }
-        LeafDesc ld{0, 0, 0, 0};
-#ifdef NICE_PROBES
-        if (act == 1 && (p.probe & 2)) {
-            ld = LeafDesc{nd.lo, nd.hi, nd.size, 0};
-        } else
-#endif
-        if (act == 1) {
-            ld = leaf_desc<MC>(nd.lo, nd.hi, nd.size, p);
-        }
-        // Leaf records: one per kLeafPiece candidates (a range without
-        // candidates still counts as an MSD-surviving range, none stored).
-        const u64 pieces64 = act == 1 ? (ld.count + kLeafPiece - 1) / kLeafPiece : 0;
-        const u32 pieces = pieces64 > 0xffffu ? 0xffffu : (u32)pieces64;
-        const u32 pos = block_reserve(&p.counters[24], pieces, slots);
-        if (act == 1) {
-            if (pieces64 > 0xffffu || (u64)pos + pieces > p.leaf_cap) {
-                atomicOr(&p.counters[25], 1u);
-            } else {
-                u64 b0_lo = ld.b0_lo, b0_hi = ld.b0_hi;
-                u64 g = ld.g0;  // residue-sequence index relative to b0
-                for (u32 q = 0; q < pieces; q++) {
-                    if (g >= p.R) {  // re-base: g < R keeps the kernel's index 32-bit
-                        const u64 cyc = g / p.R;
-                        add_u128(b0_lo, b0_hi, cyc * p.M);
-                        g -= cyc * p.R;
-                    }
-                    const u64 left = ld.count - (u64)q * kLeafPiece;
-                    const u32 cnt = left < kLeafPiece ? (u32)left : kLeafPiece;
-                    p.leaves[pos + q] = Leaf{b0_lo, b0_hi, (u32)g, cnt};
-                    g += cnt;
-                }
-            }
-            n_st++;
-            c_st += ld.count;
-            s_st += nd.size;
-        }
-        // children
-        const u32 cpos = block_reserve(&p.counters[level + 1], act == 2 ? 2u : 0u, slots);
-        if (act == 2) {
-            if (cpos + 1 >= p.q_cap) {
-                atomicOr(&p.counters[25], 1u);
-            } else {
-                const u64 half = nd.size / 2;
-                u64 m_lo = nd.lo, m_hi = nd.hi;
-                add_u128(m_lo, m_hi, half);
-                qout[cpos] = MsdNode{nd.lo, nd.hi, half, level + 1, 0u};
-                qout[cpos + 1] = MsdNode{m_lo, m_hi, nd.size - half, level + 1, 0u};
-            }
+    bool skip = false;
+    if (size != 1 && !no_skip_test) {
+        if constexpr (IsConst<G>::value) {
+            skip = p.in_range ? msd_skippable_fast<IsConst<G>::base>(lo, hi, l_lo, l_hi)
+                              : msd_skippable<G>(lo, hi, l_lo, l_hi, g);
+        } else {
+            skip = msd_skippable<G>(lo, hi, l_lo, l_hi, g);
         }
     }
+    if (skip) return 0;
+    return size < 2 * p.floor_size ? 1u : 2u;
+}
+
+// A leaf's stride-index records (one per kLeafPiece candidates; a range
+// without candidates still counts as an MSD-surviving range, none stored),
+// appended with one atomic per workgroup; statistics accumulated per lane.
+// Every thread of the workgroup calls it (act == 1: this lane has a leaf).
+template <u32 MC>
+__device__ __forceinline__ void append_leaf(const MsdLaunch &p, u32 act, u64 lo, u64 hi, u64 size,
+                                            u32 *slots, u64 &n_st, u64 &c_st, u64 &s_st) {
+    LeafDesc ld{0, 0, 0, 0};
+#ifdef NICE_PROBES
+    if (act == 1 && (p.probe & 2)) {
+        ld = LeafDesc{lo, hi, size, 0};
+    } else
+#endif
+    if (act == 1) {
+        ld = leaf_desc<MC>(lo, hi, size, p);
+    }
+    const u64 pieces64 = act == 1 ? (ld.count + kLeafPiece - 1) / kLeafPiece : 0;
+    const u32 pieces = pieces64 > 0xffffu ? 0xffffu : (u32)pieces64;
+    const u32 pos = block_reserve(&p.counters[24], pieces, slots);
+    if (act != 1) return;
+    if (pieces64 > 0xffffu || (u64)pos + pieces > p.leaf_cap) {
+        atomicOr(&p.counters[25], 1u);
+    } else {
+        u64 b0_lo = ld.b0_lo, b0_hi = ld.b0_hi;
+        u64 gi = ld.g0;  // residue-sequence index relative to b0
+        for (u32 q = 0; q < pieces; q++) {
+            if (gi >= p.R) {  // re-base: g0 < R keeps the kernel's index 32-bit
+                const u64 cyc = gi / p.R;
+                add_u128(b0_lo, b0_hi, cyc * p.M);
+                gi -= cyc * p.R;
+            }
+            const u64 left = ld.count - (u64)q * kLeafPiece;
+            const u32 cnt = left < kLeafPiece ? (u32)left : kLeafPiece;
+            p.leaves[pos + q] = Leaf{b0_lo, b0_hi, (u32)gi, cnt};
+            gi += cnt;
+        }
+    }
+    n_st++;
+    c_st += ld.count;
+    s_st += size;
+}
+
+// Workgroup statistics -> the sticky counters, one atomic each.
+__device__ __forceinline__ void flush_stats(const MsdLaunch &p, u64 n_st, u64 c_st, u64 s_st,
+                                            unsigned long long *stat) {
+    const u32 lane = threadIdx.x & 63;
     n_st = wave_sum(n_st);
     c_st = wave_sum(c_st);
     s_st = wave_sum(s_st);
@@ -425,6 +443,116 @@ msd_level_kernel(MsdLaunch p, u32 level, G g) {
         atomicAdd((unsigned long long *)(p.counters + 28), stat[1]);
         atomicAdd((unsigned long long *)(p.counters + 30), stat[2]);
     }
+}
+
+template <class G, u32 MC>
+__global__ void __launch_bounds__(256)
+msd_level_kernel(MsdLaunch p, u32 level, G g) {
+    __shared__ u32 slots[4];
+    __shared__ unsigned long long stat[3];
+    if (threadIdx.x < 3) stat[threadIdx.x] = 0;
+    const MsdNode *qin = p.q[level & 1];
+    MsdNode *qout = p.q[(level + 1) & 1];
+    const u32 n_in = p.counters[level];
+    // Workgroup-uniform loop: leaves and children are appended with one atomic
+    // per workgroup, statistics summed in LDS and added once at the end.
+    const u32 stride = gridDim.x * blockDim.x;
+    u64 n_st = 0, c_st = 0, s_st = 0;
+    for (u32 b0 = blockIdx.x * blockDim.x; b0 < n_in; b0 += stride) {
+        const u32 i = b0 + threadIdx.x;
+        u32 act = 0;  // 0 drop / idle, 1 leaf, 2 split
+        MsdNode nd{0, 0, 0, 0, 0};
+        if (i < n_in) {
+            nd = qin[i];
+            act = classify_node(p, level, nd.lo, nd.hi, nd.size, g);
+        }
+        append_leaf<MC>(p, act, nd.lo, nd.hi, nd.size, slots, n_st, c_st, s_st);
+        // children
+        const u32 cpos = block_reserve(&p.counters[level + 1], act == 2 ? 2u : 0u, slots);
+        if (act == 2) {
+            if (cpos + 1 >= p.q_cap) {
+                atomicOr(&p.counters[25], 1u);
+            } else {
+                const u64 half = nd.size / 2;
+                u64 m_lo = nd.lo, m_hi = nd.hi;
+                add_u128(m_lo, m_hi, half);
+                qout[cpos] = MsdNode{nd.lo, nd.hi, half, level + 1, 0u};
+                qout[cpos + 1] = MsdNode{m_lo, m_hi, nd.size - half, level + 1, 0u};
+            }
+        }
+    }
+    flush_stats(p, n_st, c_st, s_st, stat);
+}
+
+// The whole recursion of a chunk in ONE workgroup, level by level with
+// workgroup barriers, for chunks whose levels fit `cap` nodes (at most
+// chunk / floor: a node splits only if it holds >= 2 floor numbers).  A
+// batch is then ONE launch instead of init + up to 23 level launches --
+// each of those waited for free CUs behind the detailed kernel that runs
+// beside it, and their grids were sized for the unpruned tree.  Nodes are
+// (offset in the chunk, size) pairs in a per-workgroup ping-pong queue in
+// global memory (`scratch`: gridDim.x x 2 x cap).
+template <class G, u32 MC>
+__global__ void __launch_bounds__(256)
+msd_fused_kernel(MsdLaunch p, ChunkNode *scratch, u32 cap, G g) {
+    __shared__ u32 slots[4];
+    __shared__ u32 cnt[2];
+    __shared__ unsigned long long stat[3];
+    if (threadIdx.x < 3) stat[threadIdx.x] = 0;
+    ChunkNode *qa = scratch + (u64)blockIdx.x * 2 * cap, *qb = qa + cap;
+    u64 n_st = 0, c_st = 0, s_st = 0;
+    for (u64 ci = blockIdx.x; ci < p.nchunks; ci += gridDim.x) {
+        const u64 c = p.deal_offset + (p.first + ci) * p.deal_stride;
+        u64 clo = p.start_lo, chi = p.start_hi;
+        add_u128(clo, chi, c * p.chunk);
+        const u64 rem_lo = p.end_lo - clo;
+        const u64 rem_hi = p.end_hi - chi - (p.end_lo < clo ? 1 : 0);
+        const u32 csize = (u32)(rem_hi || rem_lo > p.chunk ? p.chunk : rem_lo);
+        if (threadIdx.x == 0) {
+            qa[0] = ChunkNode{0u, csize};
+            cnt[0] = 1;
+            cnt[1] = 0;
+        }
+        __syncthreads();
+        ChunkNode *qin = qa, *qout = qb;
+        for (u32 level = 0; level <= 22; level++) {
+            const u32 n_in = cnt[0];
+            if (n_in == 0) break;
+            for (u32 b0 = 0; b0 < n_in; b0 += 256) {
+                const u32 i = b0 + threadIdx.x;
+                u32 act = 0;
+                ChunkNode nd{0u, 0u};
+                u64 lo = clo, hi = chi;
+                if (i < n_in) {
+                    nd = qin[i];
+                    add_u128(lo, hi, nd.off);
+                    act = classify_node(p, level, lo, hi, nd.size, g);
+                }
+                append_leaf<MC>(p, act, lo, hi, nd.size, slots, n_st, c_st, s_st);
+                if (act == 2) {
+                    const u32 cp = atomicAdd(&cnt[1], 2u);
+                    if (cp + 2 > cap) {
+                        atomicOr(&p.counters[25], 1u);
+                    } else {
+                        const u32 half = nd.size / 2;
+                        qout[cp] = ChunkNode{nd.off, half};
+                        qout[cp + 1] = ChunkNode{nd.off + half, nd.size - half};
+                    }
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                cnt[0] = cnt[1] > cap ? cap : cnt[1];
+                cnt[1] = 0;
+            }
+            __syncthreads();
+            ChunkNode *t = qin;
+            qin = qout;
+            qout = t;
+        }
+        __syncthreads();  // the queues are reused by the next chunk
+    }
+    flush_stats(p, n_st, c_st, s_st, stat);
 }
 
 // ---------------------------------------------------------------------------
@@ -453,7 +581,7 @@ bool niceonly_specialised(uint32_t base) {
 }
 
 hipError_t launch_niceonly(const NiceonlyLaunch &p, int num_cus, hipStream_t s) {
-    if (!p.n_leaves_dev && p.n_leaves == 0) return hipSuccess;
+    if (!p.n_leaves_dev && p.n_leaves == 0 && !p.fin.done) return hipSuccess;
     switch (p.base) {
 #define X(b) case b: return launch_nice(p, ConstBase<b>{}, num_cus, s);
         NICE_NICEONLY_BASES(X)
@@ -484,7 +612,37 @@ static hipError_t launch_msd(const MsdLaunch &p, const G &g, int num_cus, hipStr
     return hipGetLastError();
 }
 
-hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s) {
+template <class G, u32 MC = 0>
+static hipError_t launch_fused(const MsdLaunch &p, const G &g, ChunkNode *scratch, u32 cap, u32 grid,
+                               hipStream_t s) {
+    hipLaunchKernelGGL((msd_fused_kernel<G, MC>), dim3(grid), dim3(256), 0, s, p, scratch, cap, g);
+    return hipGetLastError();
+}
+
+u32 msd_fused_cap(u64 chunk, u64 floor_size) {
+    if (chunk > 0xffffffffull || floor_size == 0) return 0;
+    const u64 need = chunk / floor_size + 2;
+    if (need > kFusedMaxCap) return 0;
+    u32 cap = 64;
+    while (cap < need) cap <<= 1;
+    return cap;
+}
+
+hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s, ChunkNode *scratch,
+                             u32 cap, u32 grid) {
+    if (scratch) {  // one workgroup per chunk, all levels in-kernel
+        if (p.nchunks > 0xffffffffull) return hipErrorInvalidValue;
+        switch (p.base) {
+        case 40:
+            if (p.in_range && p.M == 62400) return launch_fused<ConstBase<40>, 62400>(p, ConstBase<40>{}, scratch, cap, grid, s);
+            return launch_fused(p, ConstBase<40>{}, scratch, cap, grid, s);
+        case 50:
+            if (p.in_range && p.M == 122500) return launch_fused<ConstBase<50>, 122500>(p, ConstBase<50>{}, scratch, cap, grid, s);
+            return launch_fused(p, ConstBase<50>{}, scratch, cap, grid, s);
+        case 80: return launch_fused(p, ConstBase<80>{}, scratch, cap, grid, s);
+        default: return launch_fused(p, make_generic(p.base), scratch, cap, grid, s);
+        }
+    }
     switch (p.base) {
     case 40:
         if (p.in_range && p.M == 62400) return launch_msd<ConstBase<40>, 62400>(p, ConstBase<40>{}, num_cus, s);

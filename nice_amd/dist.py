@@ -319,3 +319,89 @@ def process_range_niceonly_dist(range_: FieldSize, base: int, ctx=None, group=No
             lst = shard_fn(range_.range_start, range_.range_end, base, **deal)
     rows = sorted(_gather_rows([(n, base) for n in lst], dist, group))
     return FieldResults(distribution=[], nice_numbers=[NiceNumberSimple(n, u) for n, u in rows])
+
+
+class FieldPipeline:
+    """Both modes of a stream of fields with the GPU never waiting for the
+    host: field i is submitted (detailed and niceonly on their own streams,
+    nice_*_submit) before field i-depth is collected, and -- over a
+    process group -- that field's exchange (one all-reduce, PipelinedExchange)
+    is in flight while the later fields compute.  step() returns the results of an
+    earlier field as (range, detailed FieldResults, niceonly FieldResults,
+    this rank's niceonly stats), or None while the pipeline fills; drain()
+    returns the rest.  The reference client overlaps fetch / process / submit
+    across fields the same way (client/src/main.rs:411-562).
+
+    Rank r (of N) processes the r-th contiguous detailed shard of each field
+    and is dealt every N-th niceonly chunk of it (see module doc); with
+    dist=None the whole field runs on this process's contexts."""
+
+    def __init__(self, det_ctx, nice_ctx, dist=None, group=None, depth: int = 2, **nice_opts):
+        # depth: fields kept in flight behind the one being collected (the
+        # library holds up to 3 per mode and context)
+        self.depth = depth
+        self.det, self.nice = det_ctx, nice_ctx
+        self.dist, self.group = dist, group
+        self.rank = dist.get_rank(group) if dist is not None else 0
+        self.world = dist.get_world_size(group) if dist is not None else 1
+        self.ex = PipelinedExchange(dist, group) if dist is not None else None
+        self.nice_opts = dict(nice_opts)
+        self.inflight = []  # (range, base, det ticket or None, nice ticket or None)
+        self.kernel_ms = []  # detailed kernel time of each collected field (HIP events)
+
+    def _submit(self, range_: FieldSize, base: int):
+        s, e = shard_bounds(range_.range_start, range_.range_end, self.rank, self.world)
+        opts = dict(self.nice_opts)
+        deal = niceonly_deal(range_, self.rank, self.world, opts.pop("chunk_size", 0))
+        td = self.det.detailed_submit(s, e, base) if s < e else None
+        tn = None
+        if deal:
+            opts.update(deal)
+            tn = self.nice.niceonly_submit(range_.range_start, range_.range_end, base, **opts)
+        self.inflight.append((range_, base, td, tn))
+
+    def _collect_oldest(self):
+        range_, base, td, tn = self.inflight.pop(0)
+        if td is not None:
+            hist, near = self.det.detailed_collect(td, base)
+            self.kernel_ms.append(self.det.kernel_stats().kernel_ms)
+        else:
+            hist, near = _zeros(base), []
+        nice, stats = self.nice.niceonly_collect(tn) if tn is not None else ([], None)
+        if self.ex is None:
+            return (range_, _results(hist, near, base), FieldResults(
+                distribution=[], nice_numbers=[NiceNumberSimple(n, base) for n in nice]), stats)
+        vec = list(hist[: base + 1]) + _onehot(self.rank, self.world, len(near)) \
+            + _onehot(self.rank, self.world, len(nice))
+        return self._finish(self.ex.submit(vec, (base, near, nice, stats, range_)))
+
+    def _finish(self, collected):
+        if collected is None:
+            return None
+        red, (base, near, nice, stats, range_) = collected
+        det, nic, st = finish_both(self.ex, (red, (base, near, nice, stats)))
+        return range_, det, nic, st
+
+    def step(self, range_: FieldSize, base: int):
+        self._submit(range_, base)
+        if len(self.inflight) <= self.depth:
+            return None
+        return self._collect_oldest()
+
+    def drain(self):
+        out = []
+        while self.inflight:
+            r = self._collect_oldest()
+            if r is not None:
+                out.append(r)
+        if self.ex is not None:
+            r = self._finish(self.ex.drain())
+            if r is not None:
+                out.append(r)
+        return out
+
+
+def _results(hist, near, base):
+    return FieldResults(
+        distribution=[UniquesDistributionSimple(i, hist[i]) for i in range(1, base + 1)],
+        nice_numbers=[NiceNumberSimple(n, u) for n, u in near])

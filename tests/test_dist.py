@@ -70,7 +70,39 @@ def _oracle_niceonly_shard(s, e, base, chunk_size, deal_stride=1, deal_offset=0)
 
 
 class _OracleCtx:
-    """Stands in for nice_amd.GpuContext in the CPU tests (oracle-backed)."""
+    """Stands in for nice_amd.GpuContext in the CPU tests (oracle-backed),
+    including the asynchronous submit / collect pair (two fields in flight)."""
+
+    def __init__(self):
+        self.jobs = {}
+        self.next = 0
+
+    def _ticket(self, job):
+        t = self.next
+        assert t not in self.jobs, "more than three fields in flight"
+        self.jobs[t] = job
+        self.next = (t + 1) % 3
+        return t
+
+    def detailed_submit(self, s, e, base):
+        return self._ticket(("d", s, e, base))
+
+    def detailed_collect(self, t, base):
+        _, s, e, b = self.jobs.pop(t)
+        assert b == base
+        return self.detailed_raw(s, e, base)
+
+    def niceonly_submit(self, s, e, base, **kw):
+        return self._ticket(("n", s, e, base, kw))
+
+    def niceonly_collect(self, t):
+        _, s, e, base, kw = self.jobs.pop(t)
+        return self.niceonly_raw(s, e, base, **kw)
+
+    def kernel_stats(self):
+        class _K:
+            kernel_ms = 0.0
+        return _K()
 
     def detailed_raw(self, s, e, base):
         assert s < e, "empty detailed shard must not reach the library"
@@ -132,6 +164,14 @@ def _field_worker(rank, world, port, q):
     res["tiny_both"] = ([(d.num_uniques, d.count) for d in det.distribution],
                         [(n.number, n.num_uniques) for n in det.nice_numbers],
                         [n.number for n in nic.nice_numbers])
+    # the field pipeline (bench.py's step): two fields in flight, exchange overlapped
+    pipe = D.FieldPipeline(_OracleCtx(), _OracleCtx(), dist, chunk_size=997)
+    got = [pipe.step(f, 10) for f in fields + [FieldSize(69, 70)]]
+    got = [g for g in got if g is not None] + pipe.drain()
+    res["field_pipeline"] = [((r.range_start, r.range_end),
+                              [(d.num_uniques, d.count) for d in det.distribution],
+                              [(n.number, n.num_uniques) for n in det.nice_numbers],
+                              [n.number for n in nic.nice_numbers]) for r, det, nic, _ in got]
     q.put((rank, res))
     dist.destroy_process_group()
 
@@ -167,6 +207,13 @@ def test_two_rank_field_sharding_matches_single_process():
         assert r == (w.distribution, w.nice_numbers, _oracle_niceonly_shard(a, a + 2_000, 10, 997))
     assert out[0]["pipelined"][0][2] == [69]
     assert out[0]["pipelined_both"] == out[0]["pipelined"]
+    fields = [(47, 2_047), (10 ** 6 - 53, 10 ** 6 + 1_947), (2 * 10 ** 6, 2 * 10 ** 6 + 2_000),
+              (69, 70)]
+    assert [r[0] for r in out[0]["field_pipeline"]] == fields
+    for (a, b), d, near, nice in [r for r in out[0]["field_pipeline"]]:
+        w = O.process_range_detailed(a, b, 10)
+        assert (d, near) == (w.distribution, w.nice_numbers)
+        assert nice == _oracle_niceonly_shard(a, b, 10, 997)
     w = O.process_range_detailed(69, 70, 10)
     assert out[0]["tiny"] == (w.distribution, [(69, 10)])
     assert out[0]["tiny_both"] == (w.distribution, [(69, 10)], [69])
@@ -236,3 +283,23 @@ def test_niceonly_dealing_balances_survival_skew():
     assert all(abs(c - mean) <= 0.1 * mean for c in per_rank), per_rank
     assert slabs[0] < 0.01 * mean  # the contiguous first slab is pruned
     assert sum(per_rank) == O.process_field_niceonly_ex(a, e, 50, 8, chunk=chunk)[1]
+
+
+def test_field_pipeline_single_process():
+    """FieldPipeline without a process group (bench.py at N = 1): results come
+    back `depth` fields late, in submission order, equal to the oracle."""
+    from nice_amd import dist as D
+    from nice_amd.types import FieldSize
+    from oracle import oracle as O
+    pipe = D.FieldPipeline(_OracleCtx(), _OracleCtx())
+    fields = [FieldSize(a, a + 3_000) for a in (47, 5 * 10 ** 5, 10 ** 6)]
+    got = [pipe.step(f, 10) for f in fields]
+    assert got[0] is None and got[1] is None and got[2][0] == fields[0]
+    got = got[2:] + pipe.drain()
+    assert [g[0] for g in got] == fields
+    for f, det, nic, _ in got:
+        w = O.process_range_detailed(f.range_start, f.range_end, 10)
+        assert [(d.num_uniques, d.count) for d in det.distribution] == w.distribution
+        assert [(n.number, n.num_uniques) for n in det.nice_numbers] == w.nice_numbers
+        assert [n.number for n in nic.nice_numbers] == \
+            [n for n, _ in O.process_field_niceonly_mt(f.range_start, f.range_end, 10, 2)[0].nice_numbers]

@@ -349,3 +349,125 @@ def test_both_modes_overlapped_matches_fixtures(ctx):
         assert near == [(69, 10)] and nice == [69]
     finally:
         b.close()
+
+
+@pytest.mark.parametrize("where", MSD_WHERE)
+def test_niceonly_dealt_chunks_partition_the_field(ctx, where):
+    """deal_stride / deal_offset (the N-way niceonly split, nice_amd/dist.py):
+    the N dealt runs together are the single run -- same candidates, same
+    ranges, same nice list -- for several N and chunkings, and each dealt run
+    equals the oracle over exactly its chunks."""
+    from nice_amd.dist import dealt_chunks
+    s10 = 47
+    cases = [(10, s10, 10 ** 5, 997, 3), (40, O.base_range(40)[0], O.base_range(40)[0] + 10 ** 8,
+                                          10 ** 6, 8)]
+    s50 = O.base_range(50)[0] + 7_372_000_000_000
+    cases.append((50, s50, s50 + 2 * 10 ** 9, 10 ** 7, 8))
+    for base, a, b, chunk, world in cases:
+        whole, st = ctx.niceonly_raw(a, b, base, chunk_size=chunk, msd_where=where)
+        got, cands, ranges = [], 0, 0
+        for r in range(world):
+            lst, sr = ctx.niceonly_raw(a, b, base, chunk_size=chunk, msd_where=where,
+                                       deal_stride=world, deal_offset=r)
+            got += lst
+            cands += sr.candidates
+            ranges += sr.ranges
+            if r == 1:
+                want = sum((O.process_field_niceonly_ex(cs, ce, base, 8, chunk=chunk)[1]
+                            for cs, ce in dealt_chunks(a, b, chunk, world, r)), 0)
+                assert sr.candidates == want, (base, r)
+        assert sorted(got) == whole and cands == st.candidates and ranges == st.ranges, base
+    assert ctx.niceonly_raw(47, 100, 10, chunk_size=10, deal_stride=8, deal_offset=7)[0] == []
+
+
+def test_env_msd_floor_pins_the_floor():
+    """NICE_GPU_MSD_FLOOR (client_process_gpu.rs:161-172) pins the MSD floor
+    when the caller passes none; an invalid value is ignored."""
+    import subprocess
+    import sys
+    s = O.base_range(40)[0]
+    code = ("import sys; sys.path.insert(0, %r); import nice_amd as N; c = N.GpuContext(0); "
+            "print(c.niceonly_raw(%d, %d, 40)[1].candidates)" % (ROOT, s, s + 10 ** 8))
+    def run(env_val):
+        env = dict(os.environ)
+        env.pop("NICE_GPU_MSD_FLOOR", None)
+        if env_val is not None:
+            env["NICE_GPU_MSD_FLOOR"] = env_val
+        out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True,
+                             text=True, timeout=120, check=True)
+        return int(out.stdout.strip().splitlines()[-1])
+    pinned = run("64000")
+    assert pinned == ctx_free_candidates(s, s + 10 ** 8, 64000)
+    assert run("bogus") == run(None) == ctx_free_candidates(s, s + 10 ** 8, 250)
+
+
+def ctx_free_candidates(a, b, floor):
+    c = N.GpuContext(0)
+    try:
+        return c.niceonly_raw(a, b, 40, msd_floor=floor)[1].candidates
+    finally:
+        c.close()
+
+
+def test_async_fields_match_sync(ctx):
+    """nice_detailed/niceonly_submit + _collect: three fields in flight per
+    mode, collected in any order, equal the synchronous calls; a fourth submit
+    is refused; a too-small list keeps the results for a retry."""
+    s40 = O.base_range(40)[0]
+    fa, fb = (s40, s40 + 3 * 10 ** 7), (s40 + 10 ** 9, s40 + 10 ** 9 + 2 * 10 ** 7 + 17)
+    fc = (s40 + 77, s40 + 77 + 5 * 10 ** 6)
+    want_a, want_b, want_c = (ctx.detailed_raw(*f, 40) for f in (fa, fb, fc))
+    ta = ctx.detailed_submit(*fa, 40)
+    tb = ctx.detailed_submit(*fb, 40)
+    tc = ctx.detailed_submit(*fc, 40)
+    with pytest.raises(N.NiceError):
+        ctx.detailed_submit(*fa, 40)
+    assert ctx.detailed_collect(tb, 40) == want_b
+    assert ctx.detailed_collect(tc, 40) == want_c
+    assert ctx.detailed_collect(ta, 40) == want_a
+    # near-miss lists through the async path (b10 out of range: 5 395 entries)
+    t = ctx.detailed_submit(10 ** 6, 10 ** 6 + 10 ** 4, 10)
+    lib = N._lib.lib()
+    hist = (N._lib.ctypes.c_uint64 * 11)()
+    out = (N._lib.nice_number * 10)()
+    n = N._lib.ctypes.c_size_t()
+    assert lib.nice_detailed_collect(ctx._h, t, hist, out, 10, n) == N._lib.NICE_ERR_CAPACITY
+    assert n.value == 5395
+    want = O.process_range_detailed(10 ** 6, 10 ** 6 + 10 ** 4, 10, cap=10 ** 4)
+    h, lst = ctx.detailed_collect(t, 10, cap=n.value)
+    assert lst == want.nice_numbers and [(i, h[i]) for i in range(1, 11)] == want.distribution
+    # niceonly, device and host MSD, interleaved with detailed fields
+    n1 = ctx.niceonly_submit(*fa, 40)
+    d1 = ctx.detailed_submit(*fb, 40)
+    n2 = ctx.niceonly_submit(47, 100, 10, msd_where="host")
+    assert ctx.niceonly_collect(n2)[0] == [69]
+    lst, st = ctx.niceonly_collect(n1)
+    wl, wst = ctx.niceonly_raw(*fa, 40)
+    assert lst == wl and st.candidates == wst.candidates and st.ranges == wst.ranges
+    assert ctx.detailed_collect(d1, 40) == want_b
+
+
+def test_field_pipeline_on_gpu():
+    """dist.FieldPipeline (bench.py's step) on one GPU: results one field late,
+    every field equal to the committed fixture."""
+    from nice_amd import dist as D
+    c = _oracle_fields()
+    det = next(x for x in c["detailed"] if x["name"] == "b40_extra_large_1e9")
+    nic = next(x for x in c["niceonly"] if x["name"] == "b40_extra_large_1e9")
+    a, b = N.GpuContext(0), N.GpuContext(0)
+    try:
+        pipe = D.FieldPipeline(a, b)
+        f = N.FieldSize(int(det["start"]), int(det["end"]))
+        got = [pipe.step(f, 40) for _ in range(4)]
+        got = [g for g in got if g is not None] + pipe.drain()
+        assert len(got) == 4
+        for r, d, n, st in got:
+            assert r == f
+            assert [(x.num_uniques, x.count) for x in d.distribution] == \
+                [tuple(x) for x in det["distribution"]]
+            assert [(x.number, x.num_uniques) for x in d.nice_numbers] == \
+                [(int(n_), u) for n_, u in det["near_misses"]]
+            assert st.candidates == nic["candidates"] and [x.number for x in n.nice_numbers] == []
+    finally:
+        a.close()
+        b.close()
