@@ -1,0 +1,955 @@
+// fd2_kernel.hpp -- production finite-difference detailed kernel (gfx950):
+// the device code and its per-instantiation launcher.  Instantiated per base
+// by fd2_part*.hip (compiled in parallel), driven by fd2_detailed.hip.
+//
+// Computes exactly what process_range_detailed does (common/src/
+// client_process.rs:150-191: per n the unique-digit count of n^2 and n^3 in
+// base b, histogrammed, plus the near-miss list) for segments inside a base's
+// valid range, where n^2 and n^3 have fixed digit counts D2 + D3 = b.  It
+// replaces the reference's detailed_kernel (common/src/cuda/nice_kernels.cu:
+// 486-531); the design is MI355X-first, not a translation:
+//
+//  * Each lane walks a contiguous chunk n0 .. n0+len-1 (len <= B = b^2).
+//    n^2 and n^3 live in radix-B limbs (one limb = two base-b digits) and step
+//    by finite differences, never dividing:
+//        S = n^2 += D1,            D1 = 2n + 1 += 2
+//        C = n^3 += 3 S + N3,      N3 = 3n + 1 += 3
+//    (the cube's increment 3n^2 + 3n + 1 is rebuilt from the square's limbs,
+//    so no second-order difference state is carried).  A C-limb sum is < 5B:
+//    its carry (0..4) is one multiply-high (two for b80).
+//  * Limb counts are template parameters picked by the host per segment
+//    (ND, NE = limbs of D1 = 2e+1 and E1 = 3e^2+3e+1 at the segment's end,
+//    NE2 of 6e+6 kept for the layout checks), so a step touches exactly the
+//    limbs that can change: S limbs [0, ND], C limbs [0, NE].  Carries out of
+//    those (probability ~1/B per step) and the limb-0 wraps of D1 / N3 take a
+//    rare, wave-uniform branch.
+//  * The per-step limbs are stored SCALED by the mask-table entry size ES and
+//    BIASED by 2^T - B: the stored word is directly the LDS byte address of the
+//    limb's digit-pair mask (no address arithmetic), and the radix-B carry is
+//    bit T + log2(ES) of the sum (one shift, one v_mad_i32_i24 to reduce).
+//  * n^2 mod B and n^3 mod B depend only on n mod B, so limb 0 of S and of C
+//    share ONE lookup in a low-digit table indexed by r = n0 mod B + i (< 2B:
+//    the table has 2B entries, so r never wraps inside a chunk).
+//  * Histogram: per-thread counters in LDS for a window of W unique counts
+//    around the distribution's bulk (b40: 17..32 holds all but 7e-5 of n); the
+//    rare counts outside the window (and every near-miss, which always lies
+//    above the window) take a divergent branch to a per-workgroup LDS
+//    histogram and the global near-miss list.  One flush per workgroup.
+//
+// The kernel is issue-bound on VALU and LDS together: b40 per n is 13 random
+// 8-byte LDS lookups (≈7 LDS cycles each per wave) and ≈105 VALU ops; see
+// DESIGN.md §3.1 for the cycle model and the measured roofline.
+#pragma once
+#include <stdlib.h>
+
+#include <map>
+#include <mutex>
+#include <type_traits>
+
+#include "host_math.hpp"
+#include "kernels.h"
+#include "nice_device.hpp"
+
+namespace nice {
+namespace fd2 {
+
+constexpr int log2ceil(unsigned v) { int t = 0; while ((1u << t) < v) t++; return t; }
+constexpr int ilog2(unsigned v) { int t = 0; while ((2u << t) <= v) t++; return t; }
+
+// Exactness of the digit split q = mulhi(ES v, m) = v / b over v < b^2.
+constexpr bool split_exact(unsigned base, unsigned es, unsigned long long m) {
+    for (unsigned v = 0; v < base * base; v++)
+        if (((unsigned long long)es * v * m) >> 32 != v / base) return false;
+    return true;
+}
+
+// Tuning / bottleneck-probe knobs read from the environment exist only in
+// the probe build (make -C nice_amd probe -> libnice_hip_probe.so, used by
+// scripts/); the product library ignores the environment and always runs the
+// production configuration.
+#ifdef NICE_PROBES
+static u64 probe_knob(const char *name, u64 dflt) {
+    const char *v = getenv(name);
+    return v && *v ? strtoull(v, nullptr, 10) : dflt;
+}
+#else
+static constexpr u64 probe_knob(const char *, u64 dflt) { return dflt; }
+#endif
+
+// Histogram window [W0, W0 + W) per base: where the unique-count
+// distribution of in-range n lives (scripts/fd2_windows.py, 40 000 samples
+// per base: at most 6e-4 of n fall outside; b40/50/80 keep their measured
+// production windows).  W0 + W <= cutoff + 1: every near-miss is outside.
+constexpr int window_w(int b) {
+    return b == 40 ? 15 : b == 50 ? 18 : b == 80 ? 28 : b <= 45 ? 15 : b <= 61 ? 18 : b <= 70 ? 20 : 28;
+}
+constexpr int window_w0(int b) {
+    switch (b) {
+    case 40: return 18;
+    case 42: return 19;
+    case 43: return 20;
+    case 44: case 45: case 47: return 21;
+    case 48: return 22;
+    case 49: return 23;
+    case 50: return 21;
+    case 52: return 24;
+    case 53: return 25;
+    case 54: case 55: return 26;
+    case 57: return 27;
+    case 58: return 28;
+    case 59: case 60: return 29;
+    case 62: case 63: return 30;
+    case 64: return 31;
+    case 65: return 32;
+    case 67: return 33;
+    case 68: return 34;
+    case 80: return 33;
+    default: return b * 61 / 100 - window_w(b) / 2;
+    }
+}
+
+// Waves per SIMD whose VGPR budget (512 / waves) holds a base's lane state
+// without spilling in the step loop: the stepped and cached limbs of n^2, n^3,
+// 2n+1, 3n+1 plus the mask words, R = NS + NC + 2 NX + 1 + MW registers, and
+// about as many temporaries.  b40 (R = 31) just fits 64 VGPRs (8 waves);
+// R = 35..38 (b42..50) needs ~80 (6 waves), R <= 46 (b52..60) ~96 (5),
+// wider bases 128 (4).
+constexpr int state_regs(int base) {
+    const int k = base / 5, r5 = base % 5;
+    const int d2 = r5 == 0 ? 2 * k : (r5 == 4 ? 2 * k + 2 : 2 * k + 1);
+    const int d3 = r5 == 0 ? 3 * k : (r5 == 2 ? 3 * k + 1 : 3 * k + 2);
+    const int dn = r5 == 0 ? k : k + 1;
+    return (d2 + 1) / 2 + (d3 + 1) / 2 + 2 * ((dn + 1) / 2) + 1 + (base + 31) / 32;
+}
+constexpr int state_waves(int base) {
+    const int r = state_regs(base);
+    return r <= 31 ? 8 : (r <= 38 ? 6 : (r <= 46 ? 5 : 4));
+}
+
+// In-range n fits 64 bits: BASE^DN <= 2^64 (DN digits).
+constexpr bool fits64(unsigned base, int digits) {
+    unsigned long long v = 1;
+    for (int i = 0; i < digits; i++) {
+        if (v > ~0ull / base) return false;
+        v *= base;
+    }
+    return true;
+}
+
+template <int BASE_, int ND_, int NE_, int NE2_, int PROBE_ = 0, int WG_ = 512, int VD_ = 0>
+struct Cfg {
+    static constexpr int BASE = BASE_;
+    // Bottleneck probes (timing experiments only, results are wrong): 1 = no
+    // table lookups (limb words OR-ed directly), 2 = no LDS histogram add,
+    // 4 = no limb-1 lookups of S and C.
+    static constexpr int PROBE = PROBE_;
+    static constexpr int ND = ND_, NE = NE_, NE2 = NE2_;
+    static constexpr int k = BASE / 5, r5 = BASE % 5;
+    // Digit counts inside the valid range (base_range.rs:14-32).
+    static constexpr int D2 = r5 == 0 ? 2 * k : (r5 == 4 ? 2 * k + 2 : 2 * k + 1);
+    static constexpr int D3 = r5 == 0 ? 3 * k : (r5 == 2 ? 3 * k + 1 : 3 * k + 2);
+    static constexpr int DN = r5 == 0 ? k : k + 1;
+    static constexpr bool N64 = fits64(BASE, DN);  // init's u64 path
+    static constexpr int NS = cdiv(D2, 2), NC = cdiv(D3, 2), NX = cdiv(DN, 2);
+    static constexpr int SL = ND + 1, CL = NE + 1, EL = NE2 + 1;  // per-step limbs
+    static constexpr int S_TOPD = D2 - 2 * (NS - 1), C_TOPD = D3 - 2 * (NC - 1);
+    static constexpr u32 B = (u32)BASE * BASE;
+    static constexpr int T = log2ceil(B);
+    static constexpr u32 BT = (1u << T) - B;
+    static constexpr int MW = (BASE + 31) / 32;
+    static constexpr int ES = MW == 1 ? 4 : (MW == 2 ? 8 : 16);  // table entry bytes
+    static constexpr int SH = T + ilog2(ES);                     // carry bit of a scaled limb
+    static constexpr u32 ESB = ES * B, EBT = ES * BT;
+    static constexpr int WG = WG_;
+    // Target chunk (numbers per lane), see launch_cfg: a lane's init costs a
+    // few steps, more for wider bases.
+    static constexpr int TCHUNK = BASE <= 45 ? 80 : (BASE <= 58 ? 160 : 240);
+    static constexpr int NBINS = BASE + 1;
+    // Histogram window [W0, W0 + W): per-thread counters (u32, or u16 halves
+    // shared by threads t and t + WG/2 when LDS is tight).
+    static constexpr int W = window_w(BASE);
+    static constexpr int W0 = window_w0(BASE);
+    static constexpr bool HP = true;
+    static constexpr int HROW = HP ? WG / 2 : WG;  // counters per window row
+    static constexpr int HIST_BYTES = W * HROW * 4;
+    static constexpr int OUTL = HIST_BYTES;  // per-workgroup histogram of out-of-window counts
+    // digit-pair table; at least EBT in: S limbs are stored biased by EBT and
+    // looked up at (TB - EBT) + S, an unsigned immediate offset (b65-68:
+    // EBT ~ 60 KB exceeds the histogram region, so the table starts later)
+    static constexpr int TB0 = (OUTL + 4 * NBINS + 15) / 16 * 16;
+    static constexpr int TB = TB0 >= (int)EBT ? TB0 : ((int)EBT + 15) / 16 * 16;
+    // Low-digit entry, word 1: digit bits [0, DB), then the carries and flags
+    // of the step n -> n+1, all functions of n mod B (limb 0 of S, C, D1, N3
+    // is never stored): the carry out of S limb 0 of S += D1 and the carry
+    // (0..4) out of C limb 0 of C += 3S + N3; bit 30: D1 limb-0 wrap, bit 31:
+    // N3 limb-0 wrap (top bits, so "any flag" is one compare).  Up to b52 the
+    // carries sit pre-scaled by ES = 8 (a 4-bit field at F0 holding 8 * carry,
+    // a 6-bit field at FC holding 8 * carry: one v_bfe each gives the scaled
+    // carry); b53..58 leave room only for the bare carries (1 + 3 bits, one
+    // extra multiply-add per step); wider bases have no low-digit table.
+    static constexpr int DB = BASE - 32;
+    static constexpr bool TIGHT = DB > 20;
+    static constexpr bool LSD = MW == 2 && DB > 0 && DB + (TIGHT ? 4 : 10) <= 30;
+    // (regions padded to 16 bytes: the image is copied in with 16-byte accesses)
+    static constexpr int TL = TB + ((int)(B * ES) + 15) / 16 * 16;  // low-digit table (2B entries)
+    static constexpr int LDS_BYTES = TL + (LSD ? ((int)(2 * B * ES) + 15) / 16 * 16 : 0);
+    static constexpr int TAB_BYTES = LDS_BYTES - TB;  // table image copied in per workgroup
+    static constexpr int LO = LSD ? 1 : 0;  // first stored / looked-up limb
+    static constexpr u32 DMASK = (1u << (DB > 0 && DB < 32 ? DB : 0)) - 1;
+    static constexpr u32 FLAG_D1 = 1u << 30, FLAG_N3 = 1u << 31;  // any flag: w1 >= FLAG_D1
+    static constexpr int F0 = TIGHT ? DB : (DB + 3) / 4 * 4;
+    static constexpr int FC = TIGHT ? DB + 1 : F0 + 4;
+    static constexpr int F0W = TIGHT ? 1 : 4, FCW = TIGHT ? 3 : 6;  // field widths
+    // C += 3S + N3 (N3 = 3n + 1, NN limbs).  A C limb sum is < 5B, so its
+    // carry (0..4) is a multiply-high by MAGIC = ceil(2^32 / (ES B)) (exact
+    // over the range: static_assert).
+    static constexpr int NN = NX + 1;
+    static constexpr u32 DC = ES * B;
+    static constexpr u32 MAGIC = (u32)(((1ull << 32) + DC - 1) / DC);
+    static constexpr unsigned long long TMAX = (unsigned long long)ES * (5ull * B + 4);
+    // Where one multiply-high by ceil(2^32 / (ES B)) is not exact over
+    // [0, TMAX] (b80: ES = 16), divide t / ES first (t is a multiple of ES).
+    static constexpr bool C1 = ((unsigned long long)MAGIC * DC - (1ull << 32)) * TMAX < (1ull << 32);
+    static constexpr u32 MAGICB = (u32)(((1ull << 32) + B - 1) / B);
+    // VALU-decoded limbs (no table lookup): 1 = top stepped C limb, 2 = also
+    // the top stepped S limb.  Their two digits come from one multiply-high
+    // by MAGIC_D = ceil(2^32 / (ES b)) and set their bits with 64-bit shifts,
+    // trading ~6 VALU ops for one data-random (bank-conflicting) LDS read.
+    static constexpr int VD = VD_;
+    static constexpr u32 MAGIC_D = (u32)(((1ull << 32) + ES * BASE - 1) / (ES * BASE));
+    static_assert(VD == 0 || (MW == 2 && ES == 8 && split_exact(BASE, ES, MAGIC_D)), "VALU digit split");
+    // Waves per SIMD: what the LDS allows, capped by what the lane state
+    // needs in VGPRs (the register budget is set to match, see state_waves).
+    static constexpr int WPE0 = (163840 / LDS_BYTES) * (WG / 64) / 4;
+    static constexpr int WPE1 = WPE0 < state_waves(BASE) ? WPE0 : state_waves(BASE);
+    // in whole workgroups: a workgroup puts WG / 256 waves on each SIMD
+    static constexpr int WPE = WPE1 / (WG / 256) * (WG / 256) > 0 ? WPE1 / (WG / 256) * (WG / 256) : WG / 256;
+    static_assert(WPE >= 1, "LDS: not even one workgroup fits");
+    static_assert(SL < NS && CL < NC && EL <= NE, "FD layout needs cached high limbs");
+    static_assert(ND <= NX + 1 && NE2 <= NX + 1 && NE <= NS + 1, "difference limb counts");
+    static_assert(S_TOPD >= 1 && C_TOPD >= 1, "top limb");
+    static_assert(TB >= (int)EBT && TB - (int)EBT < 65536 && (!LSD || TL < 65536), "LDS offsets");
+    static_assert(LDS_BYTES <= 163840, "LDS");
+    static_assert(TB % 16 == 0 && TAB_BYTES % 16 == 0, "16-byte table copy");
+    static_assert(W0 >= 0 && W0 + W <= NBINS, "window");
+    static_assert(!LSD || (ES == 8 && FC + FCW <= 30), "low-digit entry layout");
+    static_assert(C1 || ((unsigned long long)MAGICB * B - (1ull << 32)) * (TMAX / ES) < (1ull << 32),
+                  "C-limb carry magic");
+    static_assert(NN <= SL && NE >= NS, "C += 3S + N3 layout");
+    static_assert(3 * ES <= 64, "inline-constant multiplier");
+    static_assert((unsigned long long)NX * B * B + 2ull * B < (1ull << 32), "32-bit init columns");
+};
+
+// v_mad_u32_u24 with an inline-constant multiplier (LLVM otherwise splits it
+// into v_mul_u32_u24 + v_add3_u32).
+template <u32 K>
+__device__ __forceinline__ u32 mad_u24(u32 a, u32 c) {
+    static_assert(K <= 64, "inline constant");
+    u32 r;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "n"(K), "v"(c));
+    return r;
+}
+
+// v_bcnt_u32_b32 with a scalar accumulator: popcount(x) + acc.
+__device__ __forceinline__ u32 bcnt_acc(u32 x, u32 acc) {
+    u32 r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "s"(acc));
+    return r;
+}
+
+template <class P>
+struct State {
+    u32 S[P::NS];    // n^2: limbs [0, SL) scaled+biased, [SL, NS) plain
+    u32 C[P::NC];    // n^3: same with CL
+    u32 D1[P::ND];   // scaled, plain
+    u32 N3[P::NN];   // 3n + 1, scaled, limb i < SL offset by -3 ES BT
+    u32 r8;          // low-digit table byte offset: ES * (n mod B + i)
+    u32 hi[P::MW];   // mask of the cached (rarely changing) limbs of S and C
+};
+
+template <class P>
+__device__ __forceinline__ void or_entry(const unsigned char *p, u32 (&m)[P::MW]) {
+    if constexpr (P::MW == 1) {
+        m[0] |= *(const u32 *)p;
+    } else if constexpr (P::MW == 2) {
+        uint2 v = *(const uint2 *)p;
+        m[0] |= v.x;
+        m[1] |= v.y;
+    } else {
+        uint4 v = *(const uint4 *)p;
+        m[0] |= v.x;
+        m[1] |= v.y;
+        m[2] |= v.z;
+        // Keep the 4th (zero) dword live so the load stays ds_read_b128: LLVM
+        // would shrink it to ds_read_b96, which gfx950 serves in 8 lane groups
+        // over 32 banks (8 cycles per wave) instead of 4 groups over 64 (4).
+        asm volatile("" ::"v"(v.w));
+    }
+}
+
+// Digit bits of a scaled limb (ES = 8, v8 = 8 v, v < B) by VALU.
+template <class P>
+__device__ __forceinline__ void or_valu(u32 v8, u32 (&m)[P::MW]) {
+    const u32 q = __umulhi(v8, P::MAGIC_D);       // high digit
+    const u32 r = (v8 >> 3) - q * (u32)P::BASE;   // low digit
+    const u64 bits = (1ull << q) | (1ull << r);
+    m[0] |= (u32)bits;
+    m[1] |= (u32)(bits >> 32);
+}
+
+template <class P>
+__device__ __forceinline__ void or_plain(const unsigned char *smem, u32 v, int digits, u32 (&m)[P::MW]) {
+    if (digits == 2) {
+        or_entry<P>(smem + P::TB + v * P::ES, m);
+    } else {
+#pragma unroll
+        for (int w = 0; w < P::MW; w++) m[w] |= (v >> 5) == (u32)w ? 1u << (v & 31) : 0u;
+    }
+}
+
+template <class P>
+__device__ __forceinline__ void recompute_hi(State<P> &st, const unsigned char *smem) {
+#pragma unroll
+    for (int w = 0; w < P::MW; w++) st.hi[w] = 0;
+#pragma unroll
+    for (int i = P::SL; i < P::NS; i++) or_plain<P>(smem, st.S[i], i == P::NS - 1 ? P::S_TOPD : 2, st.hi);
+#pragma unroll
+    for (int i = P::CL; i < P::NC; i++) or_plain<P>(smem, st.C[i], i == P::NC - 1 ? P::C_TOPD : 2, st.hi);
+}
+
+// Radix-B normalisation of u64 column sums into M limbs (the value fits by the
+// host's choice of limb counts; a carry past limb M-1 is dropped).
+template <class P, int N, int M>
+__device__ __forceinline__ void normalize64(const u64 (&acc)[N], u32 (&out)[M]) {
+    u64 cy = 0;
+#pragma unroll
+    for (int t = 0; t < M; t++) {
+        u64 v = (t < N ? acc[t] : 0) + cy;
+        out[t] = (u32)(v % P::B);
+        cy = v / P::B;
+    }
+}
+
+// Radix-B normalisation of column sums into M limbs (the value fits by the
+// host's choice of limb counts; a carry past limb M-1 is dropped).  A is u32
+// where every column sum fits 32 bits (static_assert in init), else u64.
+template <class P, class A, int N, int M>
+__device__ __forceinline__ void normalize(const A (&acc)[N], u32 (&out)[M]) {
+    A cy = 0;
+#pragma unroll
+    for (int t = 0; t < M; t++) {
+        const A v = (t < N ? acc[t] : (A)0) + cy;
+        cy = v / P::B;
+        out[t] = (u32)(v - cy * P::B);
+    }
+}
+
+template <class P>
+__device__ __forceinline__ void init(State<P> &st, u64 n_lo, u64 n_hi, const unsigned char *smem) {
+    constexpr u32 B = P::B;
+    u32 X[P::NX];
+    if constexpr (P::N64) {
+        // In-range n fits 64 bits (b40 < 2^43, b50 < 2^57): two radix-B digits
+        // per u64 division by B^2, the rest in 32 bits.
+        (void)n_hi;
+        constexpr u64 B2 = (u64)B * B;
+        u64 v = n_lo;
+#pragma unroll
+        for (int j = 0; j < P::NX; j += 2) {
+            const u64 q = v / B2;
+            const u32 r = (u32)(v - q * B2);
+            X[j] = r % B;
+            if (j + 1 < P::NX) X[j + 1] = r / B;
+            v = q;
+        }
+    } else {
+        u32 w[4] = {(u32)n_lo, (u32)(n_lo >> 32), (u32)n_hi, (u32)(n_hi >> 32)};
+#pragma unroll
+        for (int j = 0; j < P::NX; j++) {
+            u64 rem = 0;
+#pragma unroll
+            for (int q = 3; q >= 0; q--) {
+                u64 cur = (rem << 32) | w[q];
+                w[q] = (u32)(cur / B);
+                rem = cur % B;
+            }
+            X[j] = (u32)rem;
+        }
+    }
+    // Column sums: at most min(NS, NX) products < B^2 plus a carry: 32 bits
+    // (Cfg static_assert).
+    using A = u32;
+    if constexpr (!P::N64) {
+        // wide bases (b80: the 1024-thread kernel at the 128-VGPR cap): u64
+        // columns, the layout whose register allocation spills least.
+        st.r8 = X[0] * P::ES;
+        {
+            u64 acc[2 * P::NX];
+#pragma unroll
+            for (int t = 0; t < 2 * P::NX; t++) acc[t] = 0;
+#pragma unroll
+            for (int i = 0; i < P::NX; i++)
+#pragma unroll
+                for (int j = 0; j < P::NX; j++) acc[i + j] += (u64)X[i] * X[j];
+            normalize64<P>(acc, st.S);
+        }
+        {
+            u64 acc[P::NS + P::NX];
+#pragma unroll
+            for (int t = 0; t < P::NS + P::NX; t++) acc[t] = 0;
+#pragma unroll
+            for (int i = 0; i < P::NS; i++)
+#pragma unroll
+                for (int j = 0; j < P::NX; j++) acc[i + j] += (u64)st.S[i] * X[j];
+            normalize64<P>(acc, st.C);
+        }
+        {
+            u64 acc[P::NX];
+#pragma unroll
+            for (int t = 0; t < P::NX; t++) acc[t] = 2ull * X[t] + (t == 0 ? 1 : 0);
+            normalize64<P>(acc, st.D1);
+        }
+        {
+            u64 acc[P::NX];
+#pragma unroll
+            for (int t = 0; t < P::NX; t++) acc[t] = 3ull * X[t] + (t == 0 ? 1 : 0);
+            normalize64<P>(acc, st.N3);
+        }
+    } else {
+        st.r8 = X[0] * P::ES;
+        {  // S = X^2
+            A acc[2 * P::NX];
+#pragma unroll
+            for (int t = 0; t < 2 * P::NX; t++) acc[t] = 0;
+#pragma unroll
+            for (int i = 0; i < P::NX; i++)
+#pragma unroll
+                for (int j = 0; j < P::NX; j++) acc[i + j] += (A)X[i] * X[j];
+            normalize<P>(acc, st.S);
+        }
+        {  // C = S * X
+            A acc[P::NS + P::NX];
+#pragma unroll
+            for (int t = 0; t < P::NS + P::NX; t++) acc[t] = 0;
+#pragma unroll
+            for (int i = 0; i < P::NS; i++)
+#pragma unroll
+                for (int j = 0; j < P::NX; j++) acc[i + j] += (A)st.S[i] * X[j];
+            normalize<P>(acc, st.C);
+        }
+        {  // D1 = 2n + 1
+            A acc[P::NX];
+#pragma unroll
+            for (int t = 0; t < P::NX; t++) acc[t] = 2 * (A)X[t] + (t == 0 ? 1 : 0);
+            normalize<P>(acc, st.D1);
+        }
+        {  // N3 = 3n + 1
+            A acc[P::NX];
+#pragma unroll
+            for (int t = 0; t < P::NX; t++) acc[t] = 3 * (A)X[t] + (t == 0 ? 1 : 0);
+            normalize<P>(acc, st.N3);
+        }
+    }
+    recompute_hi<P>(st, smem);
+    if constexpr (P::LSD) st.S[0] = st.C[0] = st.D1[0] = st.N3[0] = 0;  // from the table
+#pragma unroll
+    for (int i = 0; i < P::SL; i++) st.S[i] = (st.S[i] + P::BT) * P::ES;
+#pragma unroll
+    for (int i = 0; i < P::CL; i++) st.C[i] *= P::ES;  // unbiased: carries by multiply-high
+#pragma unroll
+    for (int i = 0; i < P::ND; i++) st.D1[i] *= P::ES;
+#pragma unroll
+    for (int i = 0; i < P::NN; i++) st.N3[i] = st.N3[i] * P::ES - (i < P::SL ? 3 * P::EBT : 0u);
+}
+
+// +ES into scaled plain limbs [from, N) (rare path).
+template <class P, int N>
+__device__ __forceinline__ void carry_scaled(u32 (&x)[N], int from) {
+    u32 c = 1;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        if (i < from) continue;
+        u32 v = x[i] + c * P::ES;
+        c = v >= P::ESB;
+        x[i] = c ? 0u : v;
+    }
+}
+// +1 into plain limbs [from, N) (rare path).
+template <class P, int N>
+__device__ __forceinline__ void carry_plain(u32 (&x)[N], int from) {
+    u32 c = 1;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        if (i < from) continue;
+        u32 v = x[i] + c;
+        c = v == P::B;
+        x[i] = c ? 0u : v;
+    }
+}
+
+// +ES into N3 limbs [1, NN) (offset limbs, rare path).
+template <class P>
+__device__ __forceinline__ void carry_n3(State<P> &st) {
+    u32 c = 1;
+#pragma unroll
+    for (int i = 1; i < P::NN; i++) {
+        const u32 off = i < P::SL ? 3 * P::EBT : 0u;
+        u32 v = st.N3[i] + off + c * P::ES;
+        c = v >= P::ESB;
+        st.N3[i] = (c ? 0u : v) - off;
+    }
+}
+
+// Rare path: a limb-0 wrap of D1 / N3, or a carry out of the top stepped
+// limb of S (tS >= 2^SH, biased) or C (tC >= ES B).  The top stepped limbs
+// are left unreduced by step(): they only take carries, so they need
+// reducing only here.
+template <class P>
+__device__ __forceinline__ void rare(State<P> &st, const unsigned char *smem, u32 d1w, u32 n3w, bool cS,
+                                     bool cC) {
+    if (d1w) carry_scaled<P>(st.D1, 1);
+    if (n3w) carry_n3<P>(st);
+    if (cS) {
+        st.S[P::SL - 1] -= P::ESB;
+        carry_plain<P>(st.S, P::SL);
+    }
+    if (cC) {
+        st.C[P::CL - 1] -= P::DC;
+        carry_plain<P>(st.C, P::CL);
+    }
+    if (cS | cC) recompute_hi<P>(st, smem);
+}
+
+// One FD step n -> n+1.  w1 = word 1 of the low-digit entry of n (LSD bases):
+// limb 0 of every quantity lives in the table, so the chains start at limb 1
+// with the table's carries.  The carry leaves each limb as c8 = ES * carry,
+// (t >> T) & ES; the limb is reduced with one v_mad_i32_i24.  The top stepped
+// limb of S and of C only ever receives a carry (D1 and 3S + N3 are shorter),
+// so it is just compared: a carry out of it (~1/B per step) goes to rare().
+template <class P>
+__device__ __forceinline__ void step(State<P> &st, const unsigned char *smem, u32 w1) {
+    constexpr u32 ES = P::ES;
+    constexpr int L0 = P::LO;  // LSD bases: limb 0 lives in the low-digit table
+    constexpr int CT = P::CL - 1, ST = P::SL - 1;  // top stepped limbs
+    static_assert(CT >= P::NS && CT >= P::NN && ST >= P::ND, "top limbs take carries only");
+    // C += 3S + N3 (old S), limbs L0 .. CL-1.  Unbiased scaled limbs; a limb
+    // sum is < 5B, its carry (0..4) is a multiply-high.
+    u32 cC = 0;
+    if constexpr (P::LSD) cC = __builtin_amdgcn_ubfe(w1, P::FC, P::FCW);  // TIGHT: bare carry
+#pragma unroll
+    for (int i = L0; i < CT; i++) {
+        u32 t;
+        if (P::TIGHT && i == L0) t = mad_u24<ES>(cC, st.C[i]);  // scale the bare carry
+        else t = st.C[i] + cC;
+        // Past limb L0 the carry is c * ES from a multiply-high: keep C + c*ES
+        // one v_lshl_add_u32 and add N3 with a plain v_add_u32 (LLVM would
+        // otherwise emit v_lshlrev_b32 + v_add3_u32, ~2 issue cycles more).
+        if (i > L0 && i < P::NN) asm("" : "+v"(t));
+        if (i < P::NN) t += st.N3[i];
+        else if (i < P::SL) t -= 3 * P::EBT;
+        // + 3S as one v_mad_u32_u24 (limbs < 2^24)
+        if (i < P::SL) t = mad_u24<3>(st.S[i], t);
+        else if (i < P::NS) t = mad_u24<3 * ES>(st.S[i], t);
+        const u32 c = P::C1 ? __umulhi(t, P::MAGIC) : __umulhi(t / ES, P::MAGICB);
+        st.C[i] = t - c * P::DC;
+        cC = c * ES;
+    }
+    st.C[CT] += cC;  // < DC + 4 ES: a carry out is at most 1
+    // S += D1, limbs L0 .. SL-1 (biased: carry = bit T of t >> log2 ES).
+    u32 cS = 0;
+    if constexpr (P::LSD) cS = __builtin_amdgcn_ubfe(w1, P::F0, P::F0W);  // TIGHT: bare carry
+#pragma unroll
+    for (int i = L0; i < ST; i++) {
+        u32 t;
+        if (P::TIGHT && i == L0) t = mad_u24<ES>(cS, st.S[i] + (i < P::ND ? st.D1[i] : 0u));
+        else t = st.S[i] + (i < P::ND ? st.D1[i] : 0u) + cS;
+        cS = (t >> P::T) & ES;
+        st.S[i] = t - cS * P::B;
+    }
+    st.S[ST] += cS;
+    st.r8 += ES;
+    const bool topS = st.S[ST] >= (1u << P::SH), topC = st.C[CT] >= P::DC;
+    if constexpr (P::LSD) {
+        if (w1 >= P::FLAG_D1 || topS || topC)
+            rare<P>(st, smem, w1 & P::FLAG_D1, w1 & P::FLAG_N3, topS, topC);
+    } else {
+        // limb 0 of D1 (+2) and N3 (+3, stored offset by -3 ES BT) step here
+        st.D1[0] += 2 * ES;
+        st.N3[0] += 3 * ES;
+        const u32 d1w = st.D1[0] >= P::ESB, n3w = st.N3[0] + 3 * P::EBT >= P::ESB;
+        if (d1w || n3w || topS || topC) {
+            if (d1w) st.D1[0] -= P::ESB;
+            if (n3w) st.N3[0] -= P::ESB;
+            rare<P>(st, smem, d1w, n3w, topS, topC);
+        }
+    }
+}
+
+// Table image (the LDS bytes from TB on): digit-pair table, entry e = d1*b +
+// d0 marks d0 and d1; low-digit table (LSD bases), entry r < 2B marks the two
+// low digits of r^2 and of r^3 (mod B) plus the limb-0 carries and wraps.
+template <class P>
+__global__ void fd2_tables_kernel(unsigned char *tb) {
+    const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= P::B) return;
+    u32 v[4] = {0, 0, 0, 0};
+    auto mark = [&](u32 x) {
+        u32 d0 = x % P::BASE, d1 = x / P::BASE;
+        v[d0 >> 5] |= 1u << (d0 & 31);
+        v[d1 >> 5] |= 1u << (d1 & 31);
+    };
+    auto put = [&](unsigned char *p) {
+        if constexpr (P::ES == 4) *(u32 *)p = v[0];
+        else if constexpr (P::ES == 8) *(uint2 *)p = make_uint2(v[0], v[1]);
+        else *(uint4 *)p = make_uint4(v[0], v[1], v[2], v[3]);
+    };
+    mark(e);
+    put(tb + e * P::ES);
+    if constexpr (P::LSD) {
+        v[0] = v[1] = v[2] = v[3] = 0;
+        const u32 B = P::B;
+        const u32 s0 = (u32)((u64)e * e % B), c0 = (u32)((u64)s0 * e % B);
+        mark(s0);
+        mark(c0);
+        const u32 d1 = (2 * e + 1) % B, n3 = (3 * e + 1) % B;
+        v[1] |= d1 + 2 >= B ? P::FLAG_D1 : 0u;                   // D1 limb-0 wrap
+        v[1] |= n3 + 3 >= B ? P::FLAG_N3 : 0u;                   // N3 limb-0 wrap
+        const u32 sc = s0 + d1 >= B ? 1u : 0u, cc = (c0 + 3 * s0 + n3) / B;
+        v[1] |= (P::TIGHT ? sc : P::ES * sc) << P::F0;            // S  += D1 carry
+        v[1] |= (P::TIGHT ? cc : P::ES * cc) << P::FC;            // C += 3S + N3 carry
+        put(tb + (P::TL - P::TB) + e * P::ES);
+        put(tb + (P::TL - P::TB) + (e + P::B) * P::ES);
+    }
+}
+
+// The table image for this device and base, built on first use (the layout
+// depends on the base only) and kept for the process.
+template <class P>
+static hipError_t fd2_tables(hipStream_t s, const uint4 **out) {
+    static std::mutex mu;
+    static std::map<int, unsigned char *> have;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = have.find(dev);
+    if (it == have.end()) {
+        unsigned char *t = nullptr;
+        if ((e = hipMalloc(&t, P::TAB_BYTES)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(t, 0, P::TAB_BYTES, s)) != hipSuccess) return e;  // padding
+        hipLaunchKernelGGL(fd2_tables_kernel<P>, dim3((P::B + 255) / 256), dim3(256), 0, s, t);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        // other streams (contexts) of this device may read it next
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        it = have.emplace(dev, t).first;
+    }
+    *out = (const uint4 *)it->second;
+    return hipSuccess;
+}
+
+// One launch covers a whole segment: blocks [0, main_blocks) walk `nunits`
+// chunks of `chunk` numbers from `start`; the blocks after them take the
+// < chunk numbers left over, one per lane, from `tail` (same code, chunk 1:
+// every parameter stays wave-uniform, and no second launch is serialised
+// behind the first).  With fin.out set, the launch also finishes the field:
+// the last workgroup to retire sums the kHistCopies histogram copies into
+// the caller's mapped result words and re-zeroes the state block, so a field
+// is ONE launch instead of main + tail + epilogue (under several fields in
+// flight each small launch waited for free CUs: 25-60 us apiece).
+struct Fd2Args {
+    u64 start_lo, start_hi;
+    u64 tail_lo, tail_hi;
+    u32 nunits, chunk;
+    u32 tail_count, main_blocks;
+    u32 cutoff;
+    u64 *hist;          // kHistCopies x 129 bins
+    NumOut out;
+    const uint4 *tabs;
+    FieldFinish fin;    // fin.out_mapped == nullptr: no in-kernel finish
+};
+
+// Last-workgroup finish (see Fd2Args).  smem is reused as scratch (>= 1 KB).
+// Hand-off without any L2 write-back (MI355X_MICROARCH.md, inter-workgroup
+// visibility: agent atomics both sides, the last arriver told by its add's
+// return value): every wave waits for its own histogram atomics
+// (vmcnt(0)), a barrier, ONE agent-scope add per workgroup; the last
+// workgroup reads the copies with agent-scope (sc1) loads.  A __threadfence()
+// here would write back and invalidate the XCD's whole L2 once per
+// workgroup: 12 000 of them made the b40 1e9 field 1.8x slower.
+template <int WG>
+__device__ __forceinline__ void field_finish(const FieldFinish &fin, u64 *hist, u32 *count,
+                                             unsigned char *smem) {
+    __shared__ u32 last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(fin.done, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    unsigned long long *acc = (unsigned long long *)smem;
+    for (u32 b = threadIdx.x; b < 129; b += WG) acc[b] = 0;
+    __syncthreads();
+    for (u32 e = threadIdx.x; e < kHistCopies * 129; e += WG) {
+        const u64 v = __hip_atomic_load(&hist[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v) {
+            atomicAdd(&acc[e % 129], (unsigned long long)v);
+            __hip_atomic_store(&hist[e], (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    for (u32 b = threadIdx.x; b < 129; b += WG) fin.out_mapped[b] = acc[b];
+    if (threadIdx.x == 0) {
+        fin.out_mapped[129] = __hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fin.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <class P>
+__device__ __forceinline__ void fd2_body(const Fd2Args &a) {
+    // Static LDS: its address is a compile-time constant, so a lookup is one
+    // ds_read with the table offset in the instruction's immediate field.
+    __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDS_BYTES];
+    u32 *hist = (u32 *)smem;
+    u32 *outl = (u32 *)(smem + P::OUTL);
+    const u32 tid = threadIdx.x;
+    const NumOut out = a.out;
+    const u32 cutoff = a.cutoff;
+    // main part or tail part of the launch (workgroup-uniform)
+    const bool main_part = blockIdx.x < a.main_blocks;
+    const u64 start_lo = main_part ? a.start_lo : a.tail_lo;
+    const u64 start_hi = main_part ? a.start_hi : a.tail_hi;
+    const u32 nunits = main_part ? a.nunits : a.tail_count;
+    const u32 chunk = main_part ? a.chunk : 1u;
+    const u32 blk = main_part ? blockIdx.x : blockIdx.x - a.main_blocks;
+    const u32 nblk = main_part ? a.main_blocks : gridDim.x - a.main_blocks;
+
+    // The tables (built once per device and base in global memory,
+    // fd2_tables) are copied in with 16-byte accesses, and the histogram
+    // region zeroed: building them here cost ~5 % of a launch of short chunks.
+    {
+        uint4 *dst = (uint4 *)(smem + P::TB);
+        for (u32 i = tid; i < (u32)(P::TAB_BYTES / 16); i += P::WG) dst[i] = a.tabs[i];
+        uint4 *h4 = (uint4 *)smem;
+        for (u32 i = tid; i < (u32)(P::TB / 16); i += P::WG) h4[i] = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+
+    // Window counters: row u - W0, column tid (u32) or tid mod WG/2 (u16 half).
+    const u32 hbase = (P::HP ? tid % P::HROW : tid) * 4;
+    const u32 hinc = P::HP && tid >= (u32)P::HROW ? 0x10000u : 1u;
+    const u32 stride = nblk * P::WG;
+    u32 probe_acc = 0;
+    for (u32 unit = blk * P::WG + tid; unit < nunits; unit += stride) {
+        u64 n0_lo = start_lo, n0_hi = start_hi;
+        add_u128(n0_lo, n0_hi, (u64)unit * chunk);
+        State<P> st;
+        init<P>(st, n0_lo, n0_hi, smem);
+        const u32 r80 = st.r8;
+        for (u32 i = 0; i < chunk; i++) {
+            u32 m[P::MW], w1 = 0;
+#pragma unroll
+            for (int w = 0; w < P::MW; w++) m[w] = st.hi[w];
+            if constexpr (P::PROBE & 1) {
+                m[0] |= st.r8;
+                w1 = st.r8 & 0xff;
+#pragma unroll
+                for (int q = P::LO; q < P::SL; q++) m[q & 1] |= st.S[q];
+#pragma unroll
+                for (int q = P::LO; q < P::CL; q++) m[q & 1] |= st.C[q];
+            } else {
+                if constexpr (P::LSD) {
+                    const uint2 v = *(const uint2 *)(smem + P::TL + st.r8);
+                    m[0] |= v.x;
+                    m[1] |= v.y & P::DMASK;
+                    w1 = v.y;
+                }
+#pragma unroll
+                for (int q = P::LO; q < P::SL; q++) {
+                    if ((P::PROBE & 4) && q == 1) { m[0] |= st.S[q] & 0xffu; continue; }  // probe: no limb-1 lookups
+                    if (P::VD >= 2 && q == P::SL - 1) or_valu<P>(st.S[q] - P::EBT, m);
+                    else or_entry<P>(smem + (P::TB - P::EBT) + st.S[q], m);
+                }
+#pragma unroll
+                for (int q = P::LO; q < P::CL; q++) {
+                    if ((P::PROBE & 4) && q == 1) { m[1] |= st.C[q] & 0xffu; continue; }
+                    if (P::VD >= 1 && q == P::CL - 1) or_valu<P>(st.C[q], m);
+                    else or_entry<P>(smem + P::TB + st.C[q], m);
+                }
+            }
+            // uw = unique count - W0: the bias rides in the first v_bcnt's
+            // accumulator operand (an SGPR; LLVM would add it separately).
+            u32 uw = bcnt_acc(m[0], (u32)(-P::W0));
+#pragma unroll
+            for (int w = 1; w < P::MW; w++) uw += __popc(m[w]);
+            if (uw < (u32)P::W) {
+                if constexpr (P::PROBE & 2) probe_acc++;
+                else atomicAdd((u32 *)(smem + uw * (P::HROW * 4) + hbase), hinc);
+            } else {
+                const u32 u = uw + P::W0;
+                atomicAdd(&outl[u], 1u);
+                if (u > cutoff) {
+                    u64 lo = n0_lo, hi = n0_hi;
+                    add_u128(lo, hi, (st.r8 - r80) / P::ES);  // = i (keeps i scalar)
+                    u32 pos = atomicAdd(out.count, 1u);
+                    if (pos < out.cap) {
+                        out.n[2 * (u64)pos] = lo;
+                        out.n[2 * (u64)pos + 1] = hi;
+                        out.u[pos] = u;
+                    }
+                }
+            }
+            step<P>(st, smem, w1);
+        }
+    }
+    if constexpr ((P::PROBE & 2) != 0) atomicAdd(&outl[P::W0], probe_acc);  // mass only
+    __syncthreads();
+    const u32 lane = tid & 63, wave = tid >> 6;
+    u64 *hist_out = a.hist + (blockIdx.x % kHistCopies) * 129;
+    for (u32 row = wave; row < (u32)P::W; row += P::WG / 64) {
+        u32 s = 0;
+#pragma unroll
+        for (int q = 0; q < P::HROW / 64; q++) {
+            const u32 v = hist[row * P::HROW + lane + 64 * q];
+            s += P::HP ? (v & 0xffffu) + (v >> 16) : v;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+        if (lane == 0 && s) atomicAdd((unsigned long long *)&hist_out[P::W0 + row], (unsigned long long)s);
+    }
+    if (tid < (u32)P::NBINS && outl[tid])
+        atomicAdd((unsigned long long *)&hist_out[tid], (unsigned long long)outl[tid]);
+    if (a.fin.out_mapped) {
+        __syncthreads();  // smem is reused by the finish
+        field_finish<P::WG>(a.fin, a.hist, out.count, smem);
+    }
+}
+
+template <class P>
+__global__ void __launch_bounds__(P::WG) __attribute__((amdgpu_waves_per_eu(P::WPE, P::WPE)))
+fd2_kernel(Fd2Args a) {
+    fd2_body<P>(a);
+}
+
+template <class P>
+static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s) {
+    auto kern = fd2_kernel<P>;
+    // Occupancy is a property of the code object: queried once per
+    // instantiation (a runtime call per launch is host latency on small fields).
+    static const int per_cu_q = [&] {
+        int v = 0;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, (const void *)kern, P::WG, 0) == hipSuccess
+                   ? v : -1;
+    }();
+    if (per_cu_q < 0) return hipErrorInvalidDeviceFunction;
+    const int per_cu = per_cu_q < 1 ? 1 : per_cu_q;
+    hipError_t e = hipSuccess;
+    // Resident lanes (one "round" of workgroups).
+    const u64 lanes = (u64)num_cus * per_cu * P::WG;
+    // u16 counters: at most 65535 numbers per lane per launch.
+    const u64 max_count = P::HP ? lanes * 60000ull : ~0ull;
+    // Every near-miss count must lie above the window (it is recorded on the
+    // out-of-window branch).
+    if (p.cutoff + 1 < (u32)(P::W0 + P::W)) return hipErrorInvalidValue;
+    // Target numbers per lane.  Short chunks put a wave's 64 lanes on nearby n,
+    // so the top stepped limbs (and the cached ones) of neighbouring lanes are
+    // equal or close and their lookups stop conflicting; a chunk still pays
+    // one init (radix-B conversion and products, ~10 steps).  Each lane takes
+    // one chunk and the grid is many rounds of workgroups, not a persistent
+    // grid: workgroups at different phases (table build, init, steps) share a
+    // CU.  b40 1e9: 2.49 ms persistent at chunk 637, 2.31 persistent at ~80,
+    // 2.19-2.21 at 60-120 non-persistent (scripts/gridx_probe.sh,
+    // profiles/r01/fd2_chunk_sweep.log).
+    const u64 tchunk = probe_knob("NICE_FD2_TCHUNK", (u64)P::TCHUNK);
+    const uint4 *tabs = nullptr;
+    if ((e = fd2_tables<P>(s, &tabs)) != hipSuccess) return e;
+    DetailedLaunch q = p;
+    u64 left = p.count;
+    while (left) {
+        const u64 cnt = left < max_count ? left : max_count;
+        // Chunk floor for fields too small to fill the chip: a lane's init
+        // costs about ten steps, but with idle CUs latency wins (b40 1e6:
+        // kernel 25 us at a floor of 32, 14 us at 4; scripts/small_fields.py).
+        const u64 min_chunk = probe_knob("NICE_FD2_MINCHUNK", 4);
+        // Whole rounds of workgroups, chunks <= the target (and <= B, the
+        // low-digit table's reach).
+        u64 rounds = (cnt + tchunk * lanes - 1) / (tchunk * lanes);
+        if (rounds < 1) rounds = 1;
+        u64 chunk = (cnt + rounds * lanes - 1) / (rounds * lanes);
+        if (chunk < min_chunk) chunk = cnt < min_chunk ? cnt : min_chunk;
+        if (chunk < 1) chunk = 1;
+        // Odd chunks: lane l of a wave then sits at n mod B = r0 + chunk * l,
+        // so its low-digit entries fall on 32 distinct bank pairs per
+        // half-wave (B is a multiple of 32 for the LSD bases).  Without a
+        // low-digit table (b80) limb 0 of n^2 and n^3 is looked up in the
+        // pair table, and a chunk divisible by 16 puts a 16-lane group on
+        // ONE bank quad for those lookups (n^2 mod 16 equal on every lane):
+        // b80 1e9 at chunk 2544 took 11.8 ms, at 2545 9.3.
+        if (chunk > 1 && chunk % 2 == 0) chunk++;
+        if (chunk > P::B) chunk = P::B % 2 ? P::B : P::B - 1;
+        const u64 nunits = cnt / chunk;
+        if (nunits > 0xffffffffull) return hipErrorInvalidValue;
+        const u64 tail = cnt - nunits * chunk;  // < chunk <= B: one number per lane
+        const u64 main_blocks = (nunits + P::WG - 1) / P::WG;  // one chunk per lane
+        const u64 tail_blocks = (tail + P::WG - 1) / P::WG;
+        Fd2Args a{};
+        a.start_lo = q.start_lo;
+        a.start_hi = q.start_hi;
+        a.tail_lo = q.start_lo;
+        a.tail_hi = q.start_hi;
+        add_u128(a.tail_lo, a.tail_hi, nunits * chunk);
+        a.nunits = (u32)nunits;
+        a.chunk = (u32)chunk;
+        a.tail_count = (u32)tail;
+        a.main_blocks = (u32)main_blocks;
+        a.cutoff = q.cutoff;
+        a.hist = q.hist;
+        a.out = q.out;
+        a.tabs = tabs;
+        // the field's finish rides on its last launch
+        a.fin = left == cnt ? q.fin : FieldFinish{nullptr, nullptr};
+        hipLaunchKernelGGL(kern, dim3((u32)(main_blocks + tail_blocks)), dim3(P::WG), 0, s, a);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        add_u128(q.start_lo, q.start_hi, cnt);
+        left -= cnt;
+    }
+    return hipSuccess;
+}
+
+
+}  // namespace fd2
+}  // namespace nice
+
+namespace nice {
+namespace fd2 {
+
+// LDS bytes / waves per SIMD of a base's kernel at a workgroup size (the
+// formulas of Cfg, evaluated without instantiating it).
+constexpr int lds_bytes(int base, int wg) {
+    const int mw = (base + 31) / 32, es = mw == 1 ? 4 : (mw == 2 ? 8 : 16), b2 = base * base;
+    const int tb0 = (window_w(base) * (wg / 2) * 4 + 4 * (base + 1) + 15) / 16 * 16;
+    int t = 0;
+    while ((1 << t) < b2) t++;
+    const int ebt = es * ((1 << t) - b2);
+    const int tb = tb0 >= ebt ? tb0 : (ebt + 15) / 16 * 16;
+    const int db = base - 32;
+    const bool lsd = mw == 2 && db > 0 && db + (db > 20 ? 4 : 10) <= 30;
+    return tb + (b2 * es + 15) / 16 * 16 + (lsd ? (2 * b2 * es + 15) / 16 * 16 : 0);
+}
+// Waves per SIMD actually resident: the LDS and VGPR caps, in whole
+// workgroups (a workgroup puts wg / 256 waves on each SIMD).
+constexpr int waves_at(int base, int wg) {
+    const int lds = (163840 / lds_bytes(base, wg)) * (wg / 64) / 4;
+    const int cap = lds < state_waves(base) ? lds : state_waves(base);
+    return cap / (wg / 256) * (wg / 256);
+}
+// Workgroup size for fields >= 1e7: the kernels are bound by LDS lookups and
+// want as many in flight as fit, so the size with more waves per SIMD under
+// the LDS budget wins, 512 on a tie.  Measured on the first three bases: b40
+// two 1024-thread workgroups per CU (8 waves/SIMD) 2.38 ms vs 2.43 for three
+// 512-thread ones (6 waves, profiles/r01/fd2_wg_sweep2.log); b80 one
+// 1024-thread workgroup (4 waves) 8.47 ms vs 9.37 at 512 (2 waves,
+// profiles/r01/b80_wg_sweep.log); b50 4 waves either way, 512 kept.
+constexpr int big_wg(int base) { return waves_at(base, 1024) > waves_at(base, 512) ? 1024 : 512; }
+
+}  // namespace fd2
+}  // namespace nice

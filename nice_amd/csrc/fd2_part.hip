@@ -1,0 +1,43 @@
+// fd2_part.hip -- per-base launchers of the FD detailed kernel, one object per
+// part (built with -DFD2_PART=k, k < FD2_NPARTS): part k instantiates the
+// bases with fd2_part_of(base) == k, so the ~70 kernel instantiations of
+// FD2_COMBOS compile in parallel.
+#include "fd2_combos.h"
+#include "fd2_kernel.hpp"
+
+#ifndef FD2_PART
+#error "build with -DFD2_PART=k"
+#endif
+
+#define FD2_CAT2(a, b) a##b
+#define FD2_CAT(a, b) FD2_CAT2(a, b)
+
+namespace nice {
+namespace fd2 {
+
+template <int B_, int ND_, int NE_, int NE2_>
+static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bool wg512, int num_cus,
+                            hipStream_t s) {
+    if constexpr (fd2_part_of(B_) != FD2_PART) {
+        return hipErrorNotFound;
+    } else {
+        if ((int)p.base != B_ || nd != ND_ || ne != NE_ || ne2 != NE2_) return hipErrorNotFound;
+        return wg512 ? launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512>>(p, num_cus, s)
+                     : launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_)>>(p, num_cus, s);
+    }
+}
+
+// hipErrorNotFound: not this part's (base, combo).
+hipError_t FD2_CAT(launch_part, FD2_PART)(const DetailedLaunch &p, int nd, int ne, int ne2, bool wg512,
+                                          int num_cus, hipStream_t s) {
+    hipError_t e;
+#define X(B_, ND_, NE_, NE2_)                                                                  \
+    if ((e = try_combo<B_, ND_, NE_, NE2_>(p, nd, ne, ne2, wg512, num_cus, s)) != hipErrorNotFound) \
+        return e;
+    FD2_COMBOS(X)
+#undef X
+    return hipErrorNotFound;
+}
+
+}  // namespace fd2
+}  // namespace nice

@@ -745,7 +745,8 @@ int nice_debug_is_nice(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t count, u
 int nice_check_is_nice_inrange(uint32_t base, uint64_t lo, uint64_t hi) {
     u128 rs, re;
     const u128 n = mk(lo, hi);
-    if (!nice::fd2_supported(base) || nice::base_range_cached(base, rs, re) != 1 || n < rs || n >= re)
+    const bool fast = base == 40 || base == 50 || base == 80;  // radix_fast.hpp instantiations
+    if (!fast || nice::base_range_cached(base, rs, re) != 1 || n < rs || n >= re)
         return fail(NICE_ERR_INVALID, "n outside the base's valid range (or base not 40/50/80)");
     switch (base) {
     case 40: return nice::is_nice_fast<40>(lo, hi) ? 1 : 0;
@@ -758,7 +759,8 @@ int nice_check_msd_skippable_inrange(uint32_t base, uint64_t slo, uint64_t shi, 
                                      uint64_t ehi) {
     u128 rs, re;
     const u128 s = mk(slo, shi), e = mk(elo, ehi);
-    if (!nice::fd2_supported(base) || nice::base_range_cached(base, rs, re) != 1 || s < rs || e > re || s >= e)
+    const bool fast = base == 40 || base == 50 || base == 80;  // radix_fast.hpp instantiations
+    if (!fast || nice::base_range_cached(base, rs, re) != 1 || s < rs || e > re || s >= e)
         return fail(NICE_ERR_INVALID, "range outside the base's valid range (or base not 40/50/80)");
     if (e - s == 1) return 0;  // a single number is never skipped (msd_prefix_filter.rs:395)
     const u128 l = e - 1;

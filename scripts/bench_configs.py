@@ -35,6 +35,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--massive-sample", type=float, default=1e11)
+    ap.add_argument("--bases", default="", help="also: detailed 1e9 at the range start of these "
+                    "bases ('all' = every FD base), with the W_alg roofline fraction")
+    ap.add_argument("--only-bases", action="store_true")
     a = ap.parse_args()
     ctx = N.GpuContext(0)
     out = []
@@ -56,6 +59,24 @@ def main():
                     "candidates_per_sec": st.candidates / sec, "nice": [str(x) for x in lst],
                     "chunk": chunk or "client rule", "note": note})
 
+    peak = 256 * 4 * 32 * 2.4e9  # int32 lane-ops/s
+    bases = []
+    if a.bases == "all":
+        bases = [b for b in range(2, 129) if N._lib.lib().nice_fd_kernel_base(b)]
+    elif a.bases:
+        bases = [int(x) for x in a.bases.split(",")]
+    for b in bases:
+        r = N.get_base_range_u128(b)
+        f = type(get_benchmark_field(BM.DEFAULT))(claim_id=0, base=b, range_start=r.range_start,
+                                                 range_end=r.range_start + 10 ** 9, range_size=10 ** 9)
+        det(f"production-b{b}-1e9", f, "range start, 1e9")
+        k = out[-1]["kernel_ms"]
+        out[-1]["roofline_frac"] = 4 * b * 10 ** 9 / (k / 1e3) / peak
+        out[-1]["w_alg_ops_per_n"] = 4 * b
+    if a.only_bases:
+        for r in out:
+            print(json.dumps(r), flush=True)
+        return
     det("base-ten", get_benchmark_field(BM.BASE_TEN), "b10 [47,100): must list (69, 10)")
     det("default", get_benchmark_field(BM.DEFAULT), "latency-dominated (SURVEY 8d)")
     det("large", get_benchmark_field(BM.LARGE))

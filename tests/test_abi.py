@@ -260,3 +260,40 @@ def test_product_library_has_no_probe_kernels():
     for knob in (b"NICE_FD2_PROBE", b"NICE_MSD_PROBE", b"NICE_FD_VARIANT", b"NICE_FD2_TCHUNK",
                  b"NICE_FD2_MINCHUNK", b"NICE_FD2_WG512", b"NICE_MSD_TRACE"):
         assert knob not in blob, knob
+
+
+FD_BASES = [40, 42, 43, 44, 45, 47, 48, 49, 50, 52, 53, 54, 55, 57, 58, 59, 60, 62, 63, 64, 65,
+            67, 68, 80]
+
+
+def test_fd_bases_and_limb_count_cuts():
+    """Every base 40..68 with a valid range (and 80) has an FD kernel; the
+    host's limb-count cuts (bignum walk, fd2_detailed.hip) equal a Python
+    restatement: the n where the radix-b^2 limb counts of 2e+1, 3e^2+3e+1 and
+    6e+6 at a segment end e change."""
+    L = _lib.lib()
+    assert [b for b in range(2, 129) if L.nice_fd_kernel_base(b)] == FD_BASES
+    for base in FD_BASES:
+        B = base * base
+
+        def limbs(x):
+            k = 0
+            while x >= B ** k:
+                k += 1
+            return k
+
+        def combo(e):
+            return (limbs(2 * e + 1), limbs(3 * e * e + 3 * e + 1), limbs(6 * e + 6))
+        s, e = O.base_range(base)
+        want, a = [], s
+        while combo(a + 1) != combo(e):
+            lo, hi, cur = a + 1, e, combo(a + 1)
+            while lo < hi:
+                mid = (lo + hi) // 2
+                lo, hi = (mid + 1, hi) if combo(mid) == cur else (lo, mid)
+            want.append(lo - 1)
+            a = lo - 1
+        buf = (ctypes.c_uint64 * 16)()
+        n = ctypes.c_size_t()
+        assert L.nice_fd_segment_cuts(base, buf, 8, n) == 0
+        assert [buf[2 * i] | (buf[2 * i + 1] << 64) for i in range(n.value)] == want, base

@@ -115,11 +115,44 @@ def test_fd_kernel_limb_count_cuts(ctx, base):
     neighbouring kernel instantiations; all must agree with the oracle."""
     cuts = _fd2_cuts(base)
     assert len(cuts) == 2
+    lib = N._lib.lib()
+    buf = (N._lib.ctypes.c_uint64 * 16)()
+    n = N._lib.ctypes.c_size_t()
+    lib.nice_fd_segment_cuts(base, buf, 8, n)
+    assert [buf[2 * i] | (buf[2 * i + 1] << 64) for i in range(n.value)] == cuts
     for c in cuts:
         check_detailed(ctx, c - 200_000, c + 200_000, base)
         check_detailed(ctx, c - 70_001, c, base)
         check_detailed(ctx, c, c + 70_001, base)
         check_detailed(ctx, c - 1, c + 2, base)
+
+
+FD_BASES_NEW = [42, 43, 44, 45, 47, 48, 49, 52, 53, 54, 55, 57, 58, 59, 60, 62, 63, 64, 65, 67, 68]
+
+
+@pytest.mark.parametrize("base", FD_BASES_NEW)
+def test_fd_kernel_production_bases(ctx, base):
+    """The FD kernel for every base 42..68 with a range (live fields are at
+    b52-54, CHANGELOG.md:21; the reference specialises a kernel per base,
+    client_process_gpu.rs:318-381): both range edges, segments straddling
+    them (generic kernel outside), every limb-count cut, a random 2e6 window
+    and ragged sizes, all against the oracle."""
+    assert N._lib.lib().nice_fd_kernel_base(base) == 1
+    s, e = O.base_range(base)
+    check_detailed(ctx, s, s + 100_000, base)
+    assert ctx.kernel_stats().fd_kernel
+    check_detailed(ctx, e - 100_000, e, base)
+    check_detailed(ctx, s - 3_000, s + 3_000, base)
+    check_detailed(ctx, e - 3_000, e + 3_000, base)
+    for c in _fd2_cuts(base):
+        check_detailed(ctx, c - 50_001, c + 50_000, base)
+        check_detailed(ctx, c - 1, c + 2, base)
+    rng = random.Random(base)
+    a = s + rng.randrange(e - s - 3 * 10 ** 6)
+    check_detailed(ctx, a, a + 2 * 10 ** 6, base,
+                   want=O.process_field_detailed_mt(a, a + 2 * 10 ** 6, base, 8))
+    for size in (1, 2, 63, 65, 257, 4097):
+        check_detailed(ctx, a + 11, a + 11 + size, base)
 
 
 def test_fd_kernel_random_windows(ctx):
@@ -471,3 +504,60 @@ def test_field_pipeline_on_gpu():
     finally:
         a.close()
         b.close()
+
+
+# --- massive config (benchmark.rs:62): b50 [start, +1e13), niceonly ----------
+def _massive():
+    p = os.path.join(ROOT, "tests", "golden", "massive_b50.json")
+    with open(p) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("where", MSD_WHERE)
+def test_massive_windows_with_candidates(ctx, where):
+    """Windows of the massive field where its candidates are (the last 3e12;
+    the MSD filter prunes the first ~70 %), on the field's own chunk grid
+    (1e8), against the oracle fixture: stride candidates, MSD-surviving
+    ranges and the nice list, for both MSD placements."""
+    m = _massive()
+    w = {int(x["start"]) - int(m["start"]): x for x in m["windows"]}
+    picks = [85 * 10 ** 11] if where == "host" else [72 * 10 ** 11, 73 * 10 ** 11, 85 * 10 ** 11,
+                                                     99 * 10 ** 11]
+    for off in picks:
+        x = w[off]
+        lst, st = ctx.niceonly_raw(int(x["start"]), int(x["end"]), 50, chunk_size=m["chunk"],
+                                   msd_where=where)
+        assert (st.candidates, st.ranges) == (x["candidates"], x["ranges"]), off
+        assert [str(n) for n in lst] == x["nice_numbers"]
+
+
+def test_massive_whole_field_sums():
+    """The whole 1e13 field on the device MSD: totals equal the sum of the
+    oracle windows (7 480 186 005 candidates, 166 585 582 ranges, no nice
+    numbers), and ten 1e12 slices sum to the same, slice by slice."""
+    m = _massive()
+    s, e = int(m["start"]), int(m["end"])
+    c = N.GpuContext(0)
+    try:
+        lst, st = c.niceonly_raw(s, e, 50)  # client chunking of a 1e13 field = 1e8
+        tot_c = sum(x["candidates"] for x in m["windows"])
+        tot_r = sum(x["ranges"] for x in m["windows"])
+        assert (st.candidates, st.ranges, lst) == (tot_c, tot_r, [])
+        assert tot_c == 7_480_186_005 and tot_r == 166_585_582
+        for k in range(10):
+            a = s + k * 10 ** 12
+            l2, s2 = c.niceonly_raw(a, a + 10 ** 12, 50, chunk_size=m["chunk"])
+            ws = [x for x in m["windows"] if a <= int(x["start"]) < a + 10 ** 12]
+            assert (s2.candidates, s2.ranges) == (sum(x["candidates"] for x in ws),
+                                                  sum(x["ranges"] for x in ws)), k
+            assert l2 == []
+        # dealt 8 ways (the N = 8 split): the same totals
+        got_c = got_r = 0
+        for r in range(8):
+            l3, s3 = c.niceonly_raw(s, e, 50, deal_stride=8, deal_offset=r)
+            got_c += s3.candidates
+            got_r += s3.ranges
+            assert l3 == []
+        assert (got_c, got_r) == (tot_c, tot_r)
+    finally:
+        c.close()

@@ -154,3 +154,24 @@ def test_scan_depth_consistent():
         d = O.scan_depth(n, 40)
         assert (d == 40) == O.is_nice(n, 40) or d == 40
     assert O.scan_depth(69, 10) == 10 and O.is_nice(69, 10)
+
+
+def test_massive_fixture_consistent():
+    """tests/golden/massive_b50.json (gen_massive_fixture.py): 100 windows of
+    1e11 tile the massive field exactly; the first 72 are pruned entirely by
+    the MSD filter; one window re-checked here with the oracle."""
+    import json
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "massive_b50.json")
+    m = json.load(open(p))
+    s = int(m["start"])
+    assert s == O.base_range(50)[0] and int(m["end"]) == s + 10 ** 13 and m["chunk"] == 10 ** 8
+    w = m["windows"]
+    assert [int(x["start"]) for x in w] == [s + i * 10 ** 11 for i in range(100)]
+    assert all(x["candidates"] == 0 for x in w[:72]) and all(x["candidates"] > 0 for x in w[73:])
+    assert sum(x["candidates"] for x in w) == 7_480_186_005
+    assert all(x["nice_numbers"] == [] for x in w)
+    # window 72 (the survival onset: 86 candidates) recomputed exactly
+    x = w[72]
+    r, c, rg = O.process_field_niceonly_ex(int(x["start"]), int(x["end"]), 50, 8, chunk=10 ** 8)
+    assert (c, rg) == (x["candidates"], x["ranges"]) == (86, x["ranges"]) and r.nice_numbers == []
