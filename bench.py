@@ -64,8 +64,8 @@ PEAK_INT32_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 78.64 Tops/s per MI355X (MI355
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="target CPU work for the bounded cpu_baseline sample")
@@ -88,15 +88,20 @@ def parse():
     return p.parse_args()
 
 
+TRAFFIC_FILES = ("profiles/r02/traffic.json", "profiles/r01/traffic.json")
+
+
 def pmc_traffic():
-    """HBM bytes per main launch of the detailed kernel, from the committed PMC
-    pass (profiles/r01/traffic.json); None if absent."""
-    p = os.path.join(ROOT, "profiles", "r01", "traffic.json")
-    try:
-        with open(p) as f:
-            return json.load(f)["bytes_per_launch"]
-    except (OSError, KeyError, ValueError):
-        return None
+    """HBM bytes per launch of the detailed kernel on the 1e9 b40 field, from
+    the newest committed PMC pass (scripts/gpu_pmc.sh -> scripts/traffic_json.py,
+    FETCH_SIZE x2 + WRITE_SIZE); (bytes, file) or (None, None)."""
+    for rel in TRAFFIC_FILES:
+        try:
+            with open(os.path.join(ROOT, rel)) as f:
+                return json.load(f)["bytes_per_launch"], rel
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
 
 
 def rank_field(base_start: int, rank: int, size: int = FIELD_SIZE):
@@ -391,7 +396,9 @@ def main():
         line["roofline"] = {
             "bound": "valu", "kernel": f"nice::fd2::fd2_kernel<Cfg<{base}, ...>>",
             "achieved": achieved, "peak": PEAK_INT32_TOPS, "unit": "int32 Tops/s",
-            "frac": achieved / PEAK_INT32_TOPS, "traffic": pmc_traffic() if default_cfg else None,
+            "frac": achieved / PEAK_INT32_TOPS,
+            "traffic": pmc_traffic()[0] if default_cfg and world == 1 else None,
+            "traffic_source": pmc_traffic()[1] if default_cfg and world == 1 else None,
             "kernel_ms": kms, "numbers_per_launch": shard,
             "work_per_unit": f"{w_alg} int32 ops per n (4 per digit x {base} digits, SURVEY 8d)",
             "pipelined_frac": step_rate / PEAK_INT32_TOPS,
@@ -401,8 +408,8 @@ def main():
                     "on the launch stream, launched back to back without overlap after the timed "
                     "region; pipelined_frac = the same work per timed step (both modes share "
                     "the GPU, consecutive fields overlap on two streams); traffic: HBM bytes per "
-                    "launch from the committed PMC pass (profiles/r01/traffic.json, FETCH_SIZE x2 "
-                    "+ WRITE_SIZE), the field's bounds are the only input",
+                    "launch from the committed PMC pass (traffic_source, FETCH_SIZE x2 + "
+                    "WRITE_SIZE), the field's bounds are the only input",
         }
     st = last_stats[0]
     if st is not None:

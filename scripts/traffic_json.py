@@ -9,7 +9,7 @@ import json
 import statistics
 import sys
 
-KERNEL = "fd2::fd2_kernel<nice::fd2::Cfg<40, 4, 8, 5, 0, 1024, 0>"
+KERNEL = "fd2::fd2_kernel<nice::fd2::Cfg<40, 4, 8, 5, 0, 1024, 0>"  # the b40 1e9 field's launch
 
 
 def per_dispatch(path, counter):
@@ -23,7 +23,7 @@ def per_dispatch(path, counter):
 fetch, nf = per_dispatch(sys.argv[1], "FETCH_SIZE")
 write, nw = per_dispatch(sys.argv[2], "WRITE_SIZE")
 out = {
-    "kernel": "nice::fd2::fd2_kernel<Cfg<40,4,8,5>> (b40 1e9 field, main launch)",
+    "kernel": "nice::fd2::fd2_kernel<Cfg<40,4,8,5>> (b40 1e9 field: one launch, tail and finish in it)",
     "fetch_size_kb": round(2 * fetch, 3),
     "write_size_kb": round(write, 3),
     "bytes_per_launch": int(round((2 * fetch + write) * 1024)),
@@ -31,6 +31,6 @@ out = {
     "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes "
               "(scripts/gpu_pmc.sh), FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 tallies "
               "128-B requests at 64 B); KB per dispatch; scripts/traffic_json.py",
-    "source": "profiles/r01/pmc_fd2_b40_traffic.csv",
+    "source": [sys.argv[1], sys.argv[2]],
 }
 print(json.dumps(out, indent=1))
