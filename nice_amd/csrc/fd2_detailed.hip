@@ -122,7 +122,30 @@ static hipError_t launch_segment(const DetailedLaunch &p, const Combo &c, int nu
         if (probe == 7) return launch_cfg<Cfg<40, 4, 8, 5, 0, 1024>>(p, num_cus, s);
         if (probe == 5) return launch_cfg<Cfg<40, 4, 8, 5, 0, 896>>(p, num_cus, s);
         if (probe == 8) return launch_cfg<Cfg<40, 4, 8, 5, 0, 512, 1>>(p, num_cus, s);
-        if (probe == 9) return launch_cfg<Cfg<40, 4, 8, 5, 0, 512, 2>>(p, num_cus, s);
+        if (probe == 9) return launch_cfg<Cfg<40, 4, 8, 5, 0, 512, 17>>(p, num_cus, s);
+    }
+    // b80 VALU-decoded limbs (probe 30 + VD: 31..34 = 1..4 top C limbs, 47 =
+    // 1 C + 1 S, 48 = 2 C + 1 S), 1024-thread workgroups, main combo
+    if (probe >= 30 && p.base == 80 && c.nd == 8 && c.ne == 16 && c.ne2 == 9) {
+        if (probe == 31) return launch_cfg<Cfg<80, 8, 16, 9, 0, 1024, 1>>(p, num_cus, s);
+        if (probe == 32) return launch_cfg<Cfg<80, 8, 16, 9, 0, 1024, 2>>(p, num_cus, s);
+        if (probe == 33) return launch_cfg<Cfg<80, 8, 16, 9, 0, 1024, 3>>(p, num_cus, s);
+        if (probe == 34) return launch_cfg<Cfg<80, 8, 16, 9, 0, 1024, 4>>(p, num_cus, s);
+        if (probe == 36) return launch_cfg<Cfg<80, 8, 16, 9, 0, 1024, 6>>(p, num_cus, s);
+        if (probe == 47) return launch_cfg<Cfg<80, 8, 16, 9, 0, 1024, 17>>(p, num_cus, s);
+        if (probe == 48) return launch_cfg<Cfg<80, 8, 16, 9, 0, 1024, 18>>(p, num_cus, s);
+    }
+    if (probe >= 30 && p.base == 64 && c.nd == 7 && c.ne == 13 && c.ne2 == 7) {
+        if (probe == 31) return launch_cfg<Cfg<64, 7, 13, 7, 0, 512, 1>>(p, num_cus, s);
+        if (probe == 32) return launch_cfg<Cfg<64, 7, 13, 7, 0, 512, 2>>(p, num_cus, s);
+        if (probe == 33) return launch_cfg<Cfg<64, 7, 13, 7, 0, 512, 3>>(p, num_cus, s);
+        if (probe == 47) return launch_cfg<Cfg<64, 7, 13, 7, 0, 512, 17>>(p, num_cus, s);
+        if (probe == 48) return launch_cfg<Cfg<64, 7, 13, 7, 0, 512, 18>>(p, num_cus, s);
+    }
+    if (probe >= 30 && p.base == 68 && c.nd == 7 && c.ne == 14 && c.ne2 == 7) {
+        if (probe == 31) return launch_cfg<Cfg<68, 7, 14, 7, 0, 1024, 1>>(p, num_cus, s);
+        if (probe == 32) return launch_cfg<Cfg<68, 7, 14, 7, 0, 1024, 2>>(p, num_cus, s);
+        if (probe == 47) return launch_cfg<Cfg<68, 7, 14, 7, 0, 1024, 17>>(p, num_cus, s);
     }
 #endif
     // Fields too small to fill the chip keep 512-thread workgroups (the

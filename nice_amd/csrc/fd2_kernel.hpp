@@ -211,13 +211,16 @@ struct Cfg {
     // [0, TMAX] (b80: ES = 16), divide t / ES first (t is a multiple of ES).
     static constexpr bool C1 = ((unsigned long long)MAGIC * DC - (1ull << 32)) * TMAX < (1ull << 32);
     static constexpr u32 MAGICB = (u32)(((1ull << 32) + B - 1) / B);
-    // VALU-decoded limbs (no table lookup): 1 = top stepped C limb, 2 = also
-    // the top stepped S limb.  Their two digits come from one multiply-high
-    // by MAGIC_D = ceil(2^32 / (ES b)) and set their bits with 64-bit shifts,
-    // trading ~6 VALU ops for one data-random (bank-conflicting) LDS read.
+    // VALU-decoded limbs (no table lookup): VD % 16 of the top stepped C
+    // limbs and VD / 16 of the top stepped S limbs.  Their two digits come
+    // from one multiply-high by MAGIC_D = ceil(2^32 / (ES b)) and set their
+    // bits with 64-bit shifts, trading VALU work (~6 ops at MW = 2, ~15 at
+    // MW = 3) for one data-random (bank-conflicting) LDS read.
     static constexpr int VD = VD_;
+    static constexpr int VDC = VD % 16, VDS = VD / 16;
     static constexpr u32 MAGIC_D = (u32)(((1ull << 32) + ES * BASE - 1) / (ES * BASE));
-    static_assert(VD == 0 || (MW == 2 && ES == 8 && split_exact(BASE, ES, MAGIC_D)), "VALU digit split");
+    static_assert(VD == 0 || (MW >= 2 && split_exact(BASE, ES, MAGIC_D)), "VALU digit split");
+    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1, "VALU-decoded limbs");
     // Waves per SIMD: what the LDS allows, capped by what the lane state
     // needs in VGPRs (the register budget is set to match, see state_waves).
     static constexpr int WPE0 = (163840 / LDS_BYTES) * (WG / 64) / 4;
@@ -287,14 +290,24 @@ __device__ __forceinline__ void or_entry(const unsigned char *p, u32 (&m)[P::MW]
     }
 }
 
-// Digit bits of a scaled limb (ES = 8, v8 = 8 v, v < B) by VALU.
+// Digit bits of a scaled limb (vs = ES v, v < B) by VALU: the high digit by
+// one multiply-high, the low one by a multiply-subtract, each bit set with a
+// 64-bit shift (digits >= 64 land in mask word 2 at MW = 3).
 template <class P>
-__device__ __forceinline__ void or_valu(u32 v8, u32 (&m)[P::MW]) {
-    const u32 q = __umulhi(v8, P::MAGIC_D);       // high digit
-    const u32 r = (v8 >> 3) - q * (u32)P::BASE;   // low digit
-    const u64 bits = (1ull << q) | (1ull << r);
-    m[0] |= (u32)bits;
-    m[1] |= (u32)(bits >> 32);
+__device__ __forceinline__ void or_valu(u32 vs, u32 (&m)[P::MW]) {
+    const u32 q = __umulhi(vs, P::MAGIC_D);                        // high digit
+    const u32 r = vs / (u32)P::ES - q * (u32)P::BASE;             // low digit
+    if constexpr (P::MW == 2) {
+        const u64 bits = (1ull << q) | (1ull << r);
+        m[0] |= (u32)bits;
+        m[1] |= (u32)(bits >> 32);
+    } else {
+        const u64 bq = 1ull << (q & 63), br = 1ull << (r & 63);
+        const u64 lo = (q < 64 ? bq : 0ull) | (r < 64 ? br : 0ull);
+        m[0] |= (u32)lo;
+        m[1] |= (u32)(lo >> 32);
+        m[2] |= (q >= 64 ? (u32)bq : 0u) | (r >= 64 ? (u32)br : 0u);
+    }
 }
 
 template <class P>
@@ -766,13 +779,13 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
 #pragma unroll
                 for (int q = P::LO; q < P::SL; q++) {
                     if ((P::PROBE & 4) && q == 1) { m[0] |= st.S[q] & 0xffu; continue; }  // probe: no limb-1 lookups
-                    if (P::VD >= 2 && q == P::SL - 1) or_valu<P>(st.S[q] - P::EBT, m);
+                    if (q >= P::SL - P::VDS) or_valu<P>(st.S[q] - P::EBT, m);
                     else or_entry<P>(smem + (P::TB - P::EBT) + st.S[q], m);
                 }
 #pragma unroll
                 for (int q = P::LO; q < P::CL; q++) {
                     if ((P::PROBE & 4) && q == 1) { m[1] |= st.C[q] & 0xffu; continue; }
-                    if (P::VD >= 1 && q == P::CL - 1) or_valu<P>(st.C[q], m);
+                    if (q >= P::CL - P::VDC) or_valu<P>(st.C[q], m);
                     else or_entry<P>(smem + P::TB + st.C[q], m);
                 }
             }
@@ -950,6 +963,24 @@ constexpr int waves_at(int base, int wg) {
 // 1024-thread workgroup (4 waves) 8.47 ms vs 9.37 at 512 (2 waves,
 // profiles/r01/b80_wg_sweep.log); b50 4 waves either way, 512 kept.
 constexpr int big_wg(int base) { return waves_at(base, 1024) > waves_at(base, 512) ? 1024 : 512; }
+
+// Limbs decoded by VALU instead of a table lookup (Cfg::VD: top C limbs +
+// 16 x top S limbs), per base where the lookups' bank conflicts outweigh the
+// VALU work: the best of VD 0/1/2/3/17 on the 1e9 field at the range start
+// (scripts/vd_sweep_all.py, profiles/r02/vd_sweep_all.log), kept where it
+// gains over ~1 %.  b64: 6.31 -> 4.67 ms (its table index n^2 mod 4096
+// keeps few residues mod 32, so the top limbs' lookups pile onto few
+// banks); b45 2.60 -> 2.41; b60 3.79 -> 3.49; b63 3.96 -> 3.68; b80 8.22 ->
+// 7.67; b40 neutral (r01).
+constexpr int valu_limbs(int base) {
+    switch (base) {
+    case 43: case 44: case 45: case 48: case 50: case 54: case 58: case 62: case 80: return 1;
+    case 53: case 63: case 64: case 65: case 68: return 2;
+    case 60: return 3;
+    case 67: return 17;
+    default: return 0;
+    }
+}
 
 }  // namespace fd2
 }  // namespace nice

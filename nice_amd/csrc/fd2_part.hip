@@ -22,8 +22,20 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
         return hipErrorNotFound;
     } else {
         if ((int)p.base != B_ || nd != ND_ || ne != NE_ || ne2 != NE2_) return hipErrorNotFound;
-        return wg512 ? launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512>>(p, num_cus, s)
-                     : launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_)>>(p, num_cus, s);
+#ifdef NICE_PROBES
+        // VALU-decoded limb sweep (scripts/vd_sweep.py): NICE_FD2_VD = 100 + VD
+        switch ((int)probe_knob("NICE_FD2_VD", 0)) {
+        case 100: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 0>>(p, num_cus, s);
+        case 101: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 1>>(p, num_cus, s);
+        case 102: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 2>>(p, num_cus, s);
+        case 103: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 3>>(p, num_cus, s);
+        case 117: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 17>>(p, num_cus, s);
+        case 118: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 18>>(p, num_cus, s);
+        default: break;
+        }
+#endif
+        return wg512 ? launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, valu_limbs(B_)>>(p, num_cus, s)
+                     : launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), valu_limbs(B_)>>(p, num_cus, s);
     }
 }
 
