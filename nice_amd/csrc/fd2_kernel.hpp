@@ -217,10 +217,15 @@ struct Cfg {
     // bits with 64-bit shifts, trading VALU work (~6 ops at MW = 2, ~15 at
     // MW = 3) for one data-random (bank-conflicting) LDS read.
     static constexpr int VD = VD_;
-    static constexpr int VDC = VD % 16, VDS = VD / 16;
+    static constexpr int VDC = VD % 16, VDS = (VD / 16) % 16;
+    // VD & 256 (no low-digit table only): limb 0 of S and of C by VALU too --
+    // n^2 mod B and n^3 mod B of a wave's lanes keep few residues mod 16, so
+    // their lookups pile onto few bank quads
+    static constexpr bool VDL = (VD & 256) != 0 && !LSD;
     static constexpr u32 MAGIC_D = (u32)(((1ull << 32) + ES * BASE - 1) / (ES * BASE));
     static_assert(VD == 0 || (MW >= 2 && split_exact(BASE, ES, MAGIC_D)), "VALU digit split");
-    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1, "VALU-decoded limbs");
+    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1 && (VD & ~0x1ff) == 0,
+                  "VALU-decoded limbs");
     // Waves per SIMD: what the LDS allows, capped by what the lane state
     // needs in VGPRs (the register budget is set to match, see state_waves).
     static constexpr int WPE0 = (163840 / LDS_BYTES) * (WG / 64) / 4;
@@ -779,13 +784,13 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
 #pragma unroll
                 for (int q = P::LO; q < P::SL; q++) {
                     if ((P::PROBE & 4) && q == 1) { m[0] |= st.S[q] & 0xffu; continue; }  // probe: no limb-1 lookups
-                    if (q >= P::SL - P::VDS) or_valu<P>(st.S[q] - P::EBT, m);
+                    if (q >= P::SL - P::VDS || (P::VDL && q == 0)) or_valu<P>(st.S[q] - P::EBT, m);
                     else or_entry<P>(smem + (P::TB - P::EBT) + st.S[q], m);
                 }
 #pragma unroll
                 for (int q = P::LO; q < P::CL; q++) {
                     if ((P::PROBE & 4) && q == 1) { m[1] |= st.C[q] & 0xffu; continue; }
-                    if (q >= P::CL - P::VDC) or_valu<P>(st.C[q], m);
+                    if (q >= P::CL - P::VDC || (P::VDL && q == 0)) or_valu<P>(st.C[q], m);
                     else or_entry<P>(smem + P::TB + st.C[q], m);
                 }
             }
@@ -968,16 +973,17 @@ constexpr int big_wg(int base) { return waves_at(base, 1024) > waves_at(base, 51
 // 16 x top S limbs), per base where the lookups' bank conflicts outweigh the
 // VALU work: the best of VD 0/1/2/3/17 on the 1e9 field at the range start
 // (scripts/vd_sweep_all.py, profiles/r02/vd_sweep_all.log), kept where it
-// gains over ~1 %.  b64: 6.31 -> 4.67 ms (its table index n^2 mod 4096
-// keeps few residues mod 32, so the top limbs' lookups pile onto few
-// banks); b45 2.60 -> 2.41; b60 3.79 -> 3.49; b63 3.96 -> 3.68; b80 8.22 ->
-// 7.67; b40 neutral (r01).
+// gains over ~1 %; without a low-digit table also limb 0 (VD & 256,
+// profiles/r02/vd_sweep_low.log).  b64: 6.31 -> 4.25 ms (its table index
+// n^2 mod 4096 keeps few residues mod 32, so lookups pile onto few banks);
+// b45 2.60 -> 2.41; b60 3.79 -> 3.41; b63 3.96 -> 3.70; b68 7.42 -> 6.87;
+// b80 8.22 -> 7.46; b40 neutral (r01).
 constexpr int valu_limbs(int base) {
     switch (base) {
-    case 43: case 44: case 45: case 48: case 50: case 54: case 58: case 62: case 80: return 1;
-    case 53: case 63: case 64: case 65: case 68: return 2;
-    case 60: return 3;
-    case 67: return 17;
+    case 43: case 44: case 45: case 48: case 50: case 54: case 58: return 1;
+    case 53: case 63: case 65: return 2;
+    case 60: case 62: case 67: case 68: case 80: return 256;  // limb 0 by VALU
+    case 64: return 258;
     default: return 0;
     }
 }

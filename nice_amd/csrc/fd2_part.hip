@@ -31,6 +31,9 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
         case 103: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 3>>(p, num_cus, s);
         case 117: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 17>>(p, num_cus, s);
         case 118: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 18>>(p, num_cus, s);
+        case 356: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 256>>(p, num_cus, s);
+        case 357: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 257>>(p, num_cus, s);
+        case 358: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 258>>(p, num_cus, s);
         default: break;
         }
 #endif

@@ -20,7 +20,8 @@ for base in bases:
     os.environ["NICE_FD2_VD"] = "0"
     ref = ctx.detailed_raw(s, s + 10 ** 9, base)
     row = []
-    for vd in (100, 101, 102, 103, 117, 0):
+    vds = [int(x) for x in os.environ.get("VDS", "100,101,102,103,117,0").split(",")]
+    for vd in vds:
         os.environ["NICE_FD2_VD"] = str(vd)
         out = ctx.detailed_raw(s, s + 10 ** 9, base)
         ts = []
