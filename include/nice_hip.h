@@ -190,7 +190,7 @@ int nice_stride_table(uint32_t base, uint32_t k, uint64_t *modulus, uint32_t *re
                       size_t cap, size_t *n_out);
 
 /* Test hooks (no device needed): the in-range fast paths of the niceonly
- * kernels (radix_fast.hpp) evaluated on the host, bases 40/50/80 with n (and
+ * kernels (radix_fast.hpp) evaluated on the host, bases 40/50/52/53/54/80 with n (and
  * [start, end)) inside the base's valid range.  is_nice: 1/0 like get_is_nice
  * (client_process.rs:222-253); msd: 1/0 like has_duplicate_msd_prefix on
  * [start, end - 1] (msd_prefix_filter.rs:382-563).  NICE_ERR_INVALID otherwise. */

@@ -700,7 +700,7 @@ __device__ __forceinline__ void field_finish(const FieldFinish &fin, u64 *hist, 
     __shared__ u32 last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(fin.done, 1u) == gridDim.x - 1;
+    if (threadIdx.x == 0) last = last_block_arrive(fin.done);
     __syncthreads();
     if (!last) return;
     unsigned long long *acc = (unsigned long long *)smem;
@@ -718,8 +718,8 @@ __device__ __forceinline__ void field_finish(const FieldFinish &fin, u64 *hist, 
     if (threadIdx.x == 0) {
         fin.out_mapped[129] = __hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(fin.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    done_reset(fin.done);
 }
 
 template <class P>

@@ -25,7 +25,7 @@ constexpr uint32_t kHistCopies = 64;
 // *done.  out_mapped == nullptr: the caller runs launch_detailed_finish.
 struct FieldFinish {
     uint64_t *out_mapped;
-    uint32_t *done;
+    uint32_t *done;  // kDoneWords arrival counters (nice_device.hpp), re-zeroed by the finish
 };
 
 struct DetailedLaunch {
@@ -75,7 +75,8 @@ struct NiceFinish {
     uint32_t *msd_mapped;          // 32 words (device MSD field end) or null
     uint32_t *count_mapped;        // nice count (field end) or null
     uint32_t *msd_counters;        // device MSD counters, or null (host MSD)
-    uint32_t *done;                // workgroups retired, re-zeroed; null: no epilogue
+    uint32_t *done;                // kDoneWords arrival counters (nice_device.hpp), re-zeroed;
+                                   // null: no epilogue
 };
 
 struct NiceonlyLaunch {

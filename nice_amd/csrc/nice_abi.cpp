@@ -41,7 +41,9 @@ namespace {
 // spread their end-of-launch atomics over the copies: hundreds of workgroups
 // adding to ONE address serialise in L2), then the two list counters.
 constexpr size_t kHistCopies = nice::kHistCopies;
-constexpr size_t kStateBytes = kHistCopies * 129 * 8 + 2 * 4;
+// (+ the detailed list count and the fd2 finish's arrival counters)
+constexpr size_t kDoneWords = 65;  // nice_device.hpp kDoneWords (device-only header)
+constexpr size_t kStateBytes = kHistCopies * 129 * 8 + (1 + kDoneWords) * 4;
 constexpr int kSlots = 3;  // fields in flight per mode and context
 
 thread_local std::string g_err;
@@ -266,8 +268,8 @@ int slot_init(Device &d, Slot &sl) {
     HIPCHK(hipHostGetDevicePointer((void **)&sl.d_msd_mapped, sl.h_msd, 0));
     HIPCHK(hipHostMalloc(&sl.h_nice, 4, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void **)&sl.d_nice_mapped, sl.h_nice, 0));
-    HIPCHK(hipMalloc(&sl.d_nice_done, 4));
-    HIPCHK(hipMemset(sl.d_nice_done, 0, 4));
+    HIPCHK(hipMalloc(&sl.d_nice_done, kDoneWords * 4));
+    HIPCHK(hipMemset(sl.d_nice_done, 0, kDoneWords * 4));
     HIPCHK(hipEventCreate(&sl.ev0));
     HIPCHK(hipEventCreate(&sl.ev1));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming));
@@ -742,16 +744,28 @@ int nice_debug_is_nice(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t count, u
     return NICE_OK;
 }
 
+// The bases with niceonly fast paths (niceonly.hip NICE_NICEONLY_BASES).
+#define NICE_FAST_BASES(X) X(40) X(50) X(52) X(53) X(54) X(80)
+static bool nice_fast_base(uint32_t base) {
+    switch (base) {
+#define X(b) case b:
+        NICE_FAST_BASES(X)
+#undef X
+        return true;
+    default: return false;
+    }
+}
+
 int nice_check_is_nice_inrange(uint32_t base, uint64_t lo, uint64_t hi) {
     u128 rs, re;
     const u128 n = mk(lo, hi);
-    const bool fast = base == 40 || base == 50 || base == 80;  // radix_fast.hpp instantiations
-    if (!fast || nice::base_range_cached(base, rs, re) != 1 || n < rs || n >= re)
+    if (!nice_fast_base(base) || nice::base_range_cached(base, rs, re) != 1 || n < rs || n >= re)
         return fail(NICE_ERR_INVALID, "n outside the base's valid range (or base not 40/50/80)");
     switch (base) {
-    case 40: return nice::is_nice_fast<40>(lo, hi) ? 1 : 0;
-    case 50: return nice::is_nice_fast<50>(lo, hi) ? 1 : 0;
-    default: return nice::is_nice_fast<80>(lo, hi) ? 1 : 0;
+#define X(b) case b: return nice::is_nice_fast<b>(lo, hi) ? 1 : 0;
+        NICE_FAST_BASES(X)
+#undef X
+    default: return NICE_ERR_INVALID;
     }
 }
 
@@ -759,16 +773,16 @@ int nice_check_msd_skippable_inrange(uint32_t base, uint64_t slo, uint64_t shi, 
                                      uint64_t ehi) {
     u128 rs, re;
     const u128 s = mk(slo, shi), e = mk(elo, ehi);
-    const bool fast = base == 40 || base == 50 || base == 80;  // radix_fast.hpp instantiations
-    if (!fast || nice::base_range_cached(base, rs, re) != 1 || s < rs || e > re || s >= e)
+    if (!nice_fast_base(base) || nice::base_range_cached(base, rs, re) != 1 || s < rs || e > re || s >= e)
         return fail(NICE_ERR_INVALID, "range outside the base's valid range (or base not 40/50/80)");
     if (e - s == 1) return 0;  // a single number is never skipped (msd_prefix_filter.rs:395)
     const u128 l = e - 1;
     const uint64_t llo = lo64(l), lhi = hi64(l);
     switch (base) {
-    case 40: return nice::msd_skippable_fast<40>(slo, shi, llo, lhi) ? 1 : 0;
-    case 50: return nice::msd_skippable_fast<50>(slo, shi, llo, lhi) ? 1 : 0;
-    default: return nice::msd_skippable_fast<80>(slo, shi, llo, lhi) ? 1 : 0;
+#define X(b) case b: return nice::msd_skippable_fast<b>(slo, shi, llo, lhi) ? 1 : 0;
+        NICE_FAST_BASES(X)
+#undef X
+    default: return NICE_ERR_INVALID;
     }
 }
 

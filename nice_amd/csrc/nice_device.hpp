@@ -201,4 +201,29 @@ static inline GenericBase make_generic(u32 base) {
     return g;
 }
 
+
+// Last-workgroup detection without one hot counter.  Every workgroup, after
+// draining its own atomics (vmcnt(0) + barrier by the caller), adds to the
+// counter of its group (blockIdx.x % kDoneGroups) in done[1 + group]; the
+// workgroup completing a group adds to done[0]; the one completing done[0]
+// is last.  A single counter hit by every workgroup serialises in L2 at
+// ~40 ns an add: ~500 workgroups ending together (a 1e6 field) cost ~20 us,
+// the niceonly kernel's ~2000 mostly idle ones ~80 us.  Every add is an
+// agent-scope RMW whose result the next one waits for, so the chain orders
+// the hand-off like a single counter (MI355X_MICROARCH.md, inter-workgroup
+// visibility).  done[] has kDoneWords words; the last workgroup re-zeroes
+// them with done_reset().  Called by thread 0; returns true in the last one.
+constexpr uint32_t kDoneGroups = 64, kDoneWords = kDoneGroups + 1;
+__device__ __forceinline__ bool last_block_arrive(uint32_t *done) {
+    const uint32_t g = blockIdx.x % kDoneGroups, n = gridDim.x;
+    const uint32_t expect = g < n ? (n - 1 - g) / kDoneGroups + 1 : 0;
+    if (atomicAdd(&done[1 + g], 1u) != expect - 1) return false;
+    const uint32_t groups = n < kDoneGroups ? n : kDoneGroups;
+    return atomicAdd(&done[0], 1u) == groups - 1;
+}
+__device__ __forceinline__ void done_reset(uint32_t *done) {
+    for (uint32_t w = threadIdx.x; w < kDoneWords; w += blockDim.x)
+        __hip_atomic_store(&done[w], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace nice

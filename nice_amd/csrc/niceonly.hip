@@ -103,7 +103,7 @@ niceonly_kernel(NiceonlyLaunch p, G g) {
         __shared__ u32 last;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0) last = atomicAdd(p.fin.done, 1u) == gridDim.x - 1;
+        if (threadIdx.x == 0) last = last_block_arrive(p.fin.done);
         __syncthreads();
         if (last) {
             // Field end (count_mapped set): results out, then the field's
@@ -123,7 +123,7 @@ niceonly_kernel(NiceonlyLaunch p, G g) {
             } else if (ctr && w == 24) {
                 __hip_atomic_store(&ctr[24], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (w == 0) __hip_atomic_store(p.fin.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            done_reset(p.fin.done);
         }
     }
 }
@@ -569,7 +569,17 @@ static hipError_t launch_nice(const NiceonlyLaunch &p, const G &g, int num_cus, 
     return hipGetLastError();
 }
 
-#define NICE_NICEONLY_BASES(X) X(40) X(50) X(80)
+// Bases with compile-time niceonly kernels (ConstBase: constant divisors in
+// the generic paths, radix_fast.hpp's in-range fast paths): the benchmark
+// bases and the live production bases (CHANGELOG.md:21).
+#define NICE_NICEONLY_BASES(X) X(40) X(50) X(52) X(53) X(54) X(80)
+
+// The k = 2 stride modulus M = (b - 1) b^2 as a compile-time constant, for
+// in-range fields whose n fit 64 bits (leaf_desc's u64 path), else 0.
+template <int B>
+constexpr u32 const_modulus() {
+    return Radix<B>::DN <= 11 && B <= 54 ? (u32)((B - 1) * B * B) : 0u;
+}
 
 bool niceonly_specialised(uint32_t base) {
     switch (base) {
@@ -633,24 +643,24 @@ hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s, Chu
     if (scratch) {  // one workgroup per chunk, all levels in-kernel
         if (p.nchunks > 0xffffffffull) return hipErrorInvalidValue;
         switch (p.base) {
-        case 40:
-            if (p.in_range && p.M == 62400) return launch_fused<ConstBase<40>, 62400>(p, ConstBase<40>{}, scratch, cap, grid, s);
-            return launch_fused(p, ConstBase<40>{}, scratch, cap, grid, s);
-        case 50:
-            if (p.in_range && p.M == 122500) return launch_fused<ConstBase<50>, 122500>(p, ConstBase<50>{}, scratch, cap, grid, s);
-            return launch_fused(p, ConstBase<50>{}, scratch, cap, grid, s);
-        case 80: return launch_fused(p, ConstBase<80>{}, scratch, cap, grid, s);
+#define X(b)                                                                                      \
+    case b:                                                                                        \
+        if (const_modulus<b>() && p.in_range && p.M == const_modulus<b>())                       \
+            return launch_fused<ConstBase<b>, const_modulus<b>()>(p, ConstBase<b>{}, scratch, cap, grid, s); \
+        return launch_fused(p, ConstBase<b>{}, scratch, cap, grid, s);
+            NICE_NICEONLY_BASES(X)
+#undef X
         default: return launch_fused(p, make_generic(p.base), scratch, cap, grid, s);
         }
     }
     switch (p.base) {
-    case 40:
-        if (p.in_range && p.M == 62400) return launch_msd<ConstBase<40>, 62400>(p, ConstBase<40>{}, num_cus, s);
-        return launch_msd(p, ConstBase<40>{}, num_cus, s);
-    case 50:
-        if (p.in_range && p.M == 122500) return launch_msd<ConstBase<50>, 122500>(p, ConstBase<50>{}, num_cus, s);
-        return launch_msd(p, ConstBase<50>{}, num_cus, s);
-    case 80: return launch_msd(p, ConstBase<80>{}, num_cus, s);
+#define X(b)                                                                          \
+    case b:                                                                            \
+        if (const_modulus<b>() && p.in_range && p.M == const_modulus<b>())           \
+            return launch_msd<ConstBase<b>, const_modulus<b>()>(p, ConstBase<b>{}, num_cus, s); \
+        return launch_msd(p, ConstBase<b>{}, num_cus, s);
+        NICE_NICEONLY_BASES(X)
+#undef X
     default: return launch_msd(p, make_generic(p.base), num_cus, s);
     }
 }

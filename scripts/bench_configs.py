@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--massive-sample", type=float, default=1e11)
     ap.add_argument("--bases", default="", help="also: detailed 1e9 at the range start of these "
                     "bases ('all' = every FD base), with the W_alg roofline fraction")
+    ap.add_argument("--nice-bases", default="", help="also: niceonly 1e10 at 1/3 of the range "
+                    "of these bases")
     ap.add_argument("--only-bases", action="store_true")
     a = ap.parse_args()
     ctx = N.GpuContext(0)
@@ -73,6 +75,12 @@ def main():
         k = out[-1]["kernel_ms"]
         out[-1]["roofline_frac"] = 4 * b * 10 ** 9 / (k / 1e3) / peak
         out[-1]["w_alg_ops_per_n"] = 4 * b
+    for b in [int(x) for x in a.nice_bases.split(",") if x]:
+        r = N.get_base_range_u128(b)
+        st = r.range_start + (r.range_end - r.range_start) // 3
+        f = type(get_benchmark_field(BM.DEFAULT))(claim_id=0, base=b, range_start=st,
+                                                 range_end=st + 10 ** 10, range_size=10 ** 10)
+        nice(f"production-b{b}-niceonly-1e10", f, note="1/3 into the range, 1e10, client chunking")
     if a.only_bases:
         for r in out:
             print(json.dumps(r), flush=True)

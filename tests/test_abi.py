@@ -168,7 +168,7 @@ def _split(x):
     return x & ((1 << 64) - 1), x >> 64
 
 
-@pytest.mark.parametrize("base", [40, 50, 80])
+@pytest.mark.parametrize("base", [40, 50, 52, 53, 54, 80])
 def test_is_nice_fast_path_matches_oracle(base):
     """radix_fast.hpp's is_nice_fast (the niceonly kernel's in-range check)
     against the oracle's get_is_nice on random in-range n, plus near-nice n
@@ -183,7 +183,7 @@ def test_is_nice_fast_path_matches_oracle(base):
     assert L.nice_check_is_nice_inrange(base, *_split(s - 1)) == _lib.NICE_ERR_INVALID
 
 
-@pytest.mark.parametrize("base", [40, 50, 80])
+@pytest.mark.parametrize("base", [40, 50, 52, 53, 54, 80])
 def test_msd_fast_path_matches_oracle(base):
     """radix_fast.hpp's msd_skippable_fast (the device MSD filter's in-range
     check) against the oracle's has_duplicate_msd_prefix, on random ranges of

@@ -222,7 +222,7 @@ MSD_WHERE = ["host", "device"]
 
 
 @pytest.mark.parametrize("where", MSD_WHERE)
-@pytest.mark.parametrize("base", [10, 12, 25, 40, 45, 62, 97])
+@pytest.mark.parametrize("base", [10, 12, 25, 40, 45, 52, 53, 54, 62, 97])
 def test_niceonly_matches_oracle(ctx, base, where):
     # client_process_gpu.rs:1500-1534: first 5e6 of each base's range
     s, e = O.base_range(base)
@@ -236,7 +236,7 @@ def test_niceonly_matches_oracle(ctx, base, where):
 @pytest.mark.parametrize("where", MSD_WHERE)
 def test_niceonly_candidate_counts(ctx, where):
     rng = random.Random(5)
-    for base in (40, 50, 80):
+    for base in (40, 50, 52, 53, 54, 80):
         s, e = O.base_range(base)
         for _ in range(3):
             a = s + rng.randrange(e - s - 10 ** 8)
