@@ -184,7 +184,7 @@ class GpuContext:
 
     def detailed_submit(self, start: int, end: int, base: int) -> int:
         """Enqueue a detailed field and return at once (a ticket for
-        detailed_collect); at most two fields in flight per context."""
+        detailed_collect); at most three fields in flight per context."""
         t = ctypes.c_int()
         check(lib().nice_detailed_submit(self._h, *_split(start), *_split(end), base, t))
         return t.value

@@ -152,7 +152,8 @@ static hipError_t launch_segment(const DetailedLaunch &p, const Combo &c, int nu
     // per-workgroup table build dominates there: b80 1e6 kernel 30 vs 38 us);
     // probe 20 forces them for b80 comparisons.
     const bool force512 = probe_knob("NICE_FD2_WG512", 0) != 0;
-    const bool wg512 = force512 || p.count < 10000000ull || (probe == 20 && p.base == 80);
+    const u64 small = probe_knob("NICE_FD2_SMALL", 10000000ull);  // probe: small-field threshold
+    const bool wg512 = force512 || p.count < small || (probe == 20 && p.base == 80);
     using Fn = hipError_t (*)(const DetailedLaunch &, int, int, int, bool, int, hipStream_t);
     static const Fn parts[FD2_NPARTS] = {launch_part0, launch_part1, launch_part2,
                                          launch_part3, launch_part4, launch_part5};

@@ -22,10 +22,13 @@ constexpr uint32_t kHistCopies = 64;
 // In-kernel end of a field (fd2 kernels): the launch's last workgroup sums
 // the histogram copies into out_mapped[0..128] (mapped host memory), writes
 // the near-miss count to out_mapped[129] and re-zeroes copies, count and
-// *done.  out_mapped == nullptr: the caller runs launch_detailed_finish.
+// *done; then, after a system-scope release, seq to out_mapped[130], which the
+// host polls instead of waiting for the kernel's completion signal.
+// out_mapped == nullptr: the caller runs launch_detailed_finish.
 struct FieldFinish {
     uint64_t *out_mapped;
     uint32_t *done;  // kDoneWords arrival counters (nice_device.hpp), re-zeroed by the finish
+    uint64_t seq;    // the field's sequence number (nonzero)
 };
 
 struct DetailedLaunch {

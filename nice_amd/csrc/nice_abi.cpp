@@ -45,11 +45,35 @@ constexpr size_t kHistCopies = nice::kHistCopies;
 constexpr size_t kDoneWords = 65;  // nice_device.hpp kDoneWords (device-only header)
 constexpr size_t kStateBytes = kHistCopies * 129 * 8 + (1 + kDoneWords) * 4;
 constexpr int kSlots = 3;  // fields in flight per mode and context
+constexpr size_t kFinWords = 132;  // Slot::h_fin
 
 thread_local std::string g_err;
 
 // Slots a context rotates through (probe build: NICE_SLOTS limits it, for
 // pipeline-depth experiments).
+// How collect waits for a detailed field that ends in fd2's in-kernel finish:
+// by polling the sequence word it publishes in mapped memory (default), or
+// (probe build: NICE_SPIN=0) by the stream's completion event.
+inline bool spin_wait() {
+#ifdef NICE_PROBES
+    static const bool v = !getenv("NICE_SPIN") || atoi(getenv("NICE_SPIN")) != 0;
+    return v;
+#else
+    return true;
+#endif
+}
+
+// Probe build: NICE_NOTIME=1 skips the start event of a detailed field,
+// 2 also records its end on a non-timing event (kernel_ms reads 0).
+inline int no_time() {
+#ifdef NICE_PROBES
+    static const int v = getenv("NICE_NOTIME") ? atoi(getenv("NICE_NOTIME")) : 0;
+    return v;
+#else
+    return 0;
+#endif
+}
+
 inline int slots_used() {
 #ifdef NICE_PROBES
     static const int n = getenv("NICE_SLOTS") ? std::max(1, std::min(kSlots, atoi(getenv("NICE_SLOTS")))) : kSlots;
@@ -119,7 +143,8 @@ struct Slot {
     uint32_t *d_count = nullptr;  // detailed list count
     uint32_t *d_done = nullptr;   // workgroups retired (fd2's in-kernel finish)
     uint32_t *d_nice_count = nullptr;  // niceonly list count
-    uint64_t *h_fin = nullptr;    // mapped pinned: summed histogram [0..128], near-miss count [129]
+    uint64_t *h_fin = nullptr;    // mapped pinned: summed histogram [0..128], near-miss count [129],
+                                  // sequence word [130] (kFinWords)
     uint64_t *d_fin = nullptr;    // device view of h_fin
     ListBuf det, nice;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_done = nullptr, nice_done = nullptr;
@@ -128,6 +153,8 @@ struct Slot {
     uint32_t *d_msd_mapped = nullptr, *d_nice_mapped = nullptr;  // device views
     uint32_t *d_nice_done = nullptr;  // workgroups retired (niceonly in-kernel finish)
     bool dirty = true;            // state block not known to be zero
+    uint64_t seq = 0;             // last detailed field's sequence number
+    bool fin_seq = false;         // ... and whether its fd2 finish publishes it
     MsdBuf msd;
 };
 
@@ -141,6 +168,7 @@ struct Device {
     LeafBuf desc[2];
     int desc_next = 0;
     nice_kernel_stats last{};
+    int stats_slot = -1;  // slot whose events last.kernel_ms is still to be read from
 };
 
 struct StrideCache {
@@ -262,7 +290,8 @@ int slot_init(Device &d, Slot &sl) {
     HIPCHK(hipMalloc(&sl.d_state, kStateBytes));
     sl.d_count = (uint32_t *)(sl.d_state + kHistCopies * 129);
     sl.d_done = sl.d_count + 1;
-    HIPCHK(hipHostMalloc(&sl.h_fin, 130 * 8, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostMalloc(&sl.h_fin, kFinWords * 8, hipHostMallocMapped | hipHostMallocCoherent));
+    memset(sl.h_fin, 0, kFinWords * 8);
     HIPCHK(hipHostGetDevicePointer((void **)&sl.d_fin, sl.h_fin, 0));
     HIPCHK(hipHostMalloc(&sl.h_msd, 32 * 4, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void **)&sl.d_msd_mapped, sl.h_msd, 0));
@@ -415,7 +444,11 @@ int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *f
             p.count = c;
             // the field's last launch finishes it when it is an fd2 launch
             const bool last = a + c == e;
-            p.fin = last && fd ? nice::FieldFinish{sl.d_fin, sl.d_done} : nice::FieldFinish{nullptr, nullptr};
+            p.fin = last && fd ? nice::FieldFinish{sl.d_fin, sl.d_done, sl.seq}
+                               : nice::FieldFinish{nullptr, nullptr, 0};
+#ifdef NICE_PROBES
+            if (getenv("NICE_FD2_NOFIN")) p.fin = nice::FieldFinish{nullptr, nullptr, 0};  // probe: finish kernel
+#endif
 #ifdef NICE_PROBES
             const int var = fd_variant();
             const bool fd2 = fd && var == 0 && nice::fd2_supported(base);
@@ -429,7 +462,7 @@ int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *f
 #endif
             if (err != hipSuccess)
                 return fail(NICE_ERR_HIP, std::string("detailed launch: ") + hipGetErrorString(err));
-            if (last) *finished = fd2;
+            if (last) *finished = fd2 && p.fin.out_mapped;
             a += c;
             cnt -= c;
         }
@@ -449,20 +482,73 @@ int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *f
     return launch(std::max(s, re), e, false);
 }
 
+// The event after a detailed field's last launch: the kernel end (ev1) when
+// fd2 finished the field in-kernel, else the finish kernel's (ev_done).
+inline hipEvent_t done_event(const Slot &sl) { return sl.fin_seq && no_time() != 2 ? sl.ev1 : sl.ev_done; }
+
+// The kernel time of the device's last collected field, read from its slot's
+// events on demand (collect returns as soon as the results are published,
+// possibly before the end-of-kernel event has completed).
+int resolve_stats(Device &d) {
+    if (d.stats_slot < 0) return NICE_OK;
+    Slot &sl = d.slot[d.stats_slot];
+    d.stats_slot = -1;
+    HIPCHK(hipSetDevice(d.id));
+    HIPCHK(hipEventSynchronize(done_event(sl)));
+    float ms = 0;
+    if (!no_time()) HIPCHK(hipEventElapsedTime(&ms, sl.ev0, sl.ev1));
+    d.last.kernel_ms = ms;
+    return NICE_OK;
+}
+
+// Wait until the detailed field in slot `sl` is finished.  A field ending in
+// fd2's in-kernel finish is waited for by polling the sequence word that
+// finish publishes in mapped memory -- microseconds sooner than the kernel's
+// completion signal (which still follows: the last workgroup retires after
+// publishing).  The completion event is queried every 4096 polls, so a failed
+// launch or a finish that never publishes is reported, not spun on.
+int wait_field(Slot &sl) {
+    if (!sl.fin_seq || !spin_wait()) {
+        HIPCHK(hipEventSynchronize(done_event(sl)));
+        return NICE_OK;
+    }
+    for (uint32_t i = 1;; i++) {
+        if (__atomic_load_n(&sl.h_fin[130], __ATOMIC_ACQUIRE) == sl.seq) return NICE_OK;
+        if ((i & 4095) == 0) {
+            const hipError_t q = hipEventQuery(done_event(sl));
+            if (q == hipSuccess) {
+                if (__atomic_load_n(&sl.h_fin[130], __ATOMIC_ACQUIRE) == sl.seq) return NICE_OK;
+                return fail(NICE_ERR_HIP, "detailed field completed without publishing its results");
+            }
+            if (q != hipErrorNotReady) return fail(NICE_ERR_HIP, std::string("detailed field: ") + hipGetErrorString(q));
+        }
+        __builtin_ia32_pause();
+    }
+}
+
 // Enqueue one device's shard of a detailed field into slot `sl` (async).
 int enqueue_detailed_shard(Device &d, Slot &sl, u128 s, u128 e, uint32_t base) {
     HIPCHK(hipSetDevice(d.id));
+    // this slot's events are about to be re-recorded
+    if (d.stats_slot == (int)(&sl - d.slot)) {
+        int rc = resolve_stats(d);
+        if (rc) return rc;
+    }
+    sl.seq++;
     // The state block is zeroed by the previous field's finish; a memset
     // only after an interrupted field (or the first one).
     if (sl.dirty) HIPCHK(hipMemsetAsync(sl.d_state, 0, kStateBytes, sl.stream));
     sl.dirty = true;
-    HIPCHK(hipEventRecord(sl.ev0, sl.stream));
+    if (!no_time()) HIPCHK(hipEventRecord(sl.ev0, sl.stream));
     bool finished = false;
     int rc = enqueue_detailed(d, sl, s, e, base, &finished);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(sl.ev1, sl.stream));
-    if (!finished) HIPCHK(nice::launch_detailed_finish(sl.d_state, sl.d_count, sl.d_fin, sl.stream));
-    HIPCHK(hipEventRecord(sl.ev_done, sl.stream));
+    HIPCHK(hipEventRecord(no_time() == 2 ? sl.ev_done : sl.ev1, sl.stream));
+    sl.fin_seq = finished;
+    if (!finished) {
+        HIPCHK(nice::launch_detailed_finish(sl.d_state, sl.d_count, sl.d_fin, sl.stream));
+        HIPCHK(hipEventRecord(sl.ev_done, sl.stream));
+    }
     return NICE_OK;
 }
 
@@ -502,13 +588,13 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
         Device &d = ctx->devs[i];
         Slot &sl = d.slot[t];
         d.last = nice_kernel_stats{};
+        d.stats_slot = -1;
         if (job.bounds[i] >= job.bounds[i + 1]) continue;
         HIPCHK(hipSetDevice(d.id));
-        HIPCHK(hipEventSynchronize(sl.ev_done));
+        int rc = wait_field(sl);
+        if (rc) return rc;
         sl.dirty = false;  // the epilogue zeroed the state block
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, sl.ev0, sl.ev1));
-        d.last.kernel_ms = ms;
+        d.stats_slot = t;  // kernel_ms read on demand (resolve_stats)
         d.last.numbers = (uint64_t)(job.bounds[i + 1] - job.bounds[i]);
         d.last.launches = 1;
         d.last.fd_kernel = nice::fd2_supported(base) ? 1u : 0u;
@@ -517,16 +603,20 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
             // Near-miss list overflowed (e.g. out-of-range n, SURVEY hazard 9):
             // grow to the exact count and redo this shard (behind any field
             // queued after it; only this slot's completion is awaited).
-            int rc = ensure_listbuf(d, sl.det, cnt, true);
+            rc = ensure_listbuf(d, sl.det, cnt, true);
             if (!rc) rc = enqueue_detailed_shard(d, sl, job.bounds[i], job.bounds[i + 1], base);
+            if (!rc) rc = wait_field(sl);
             if (rc) return rc;
-            HIPCHK(hipEventSynchronize(sl.ev_done));
             sl.dirty = false;
+            d.stats_slot = t;
             cnt = (uint32_t)sl.h_fin[129];
             if (cnt > sl.det.cap) return fail(NICE_ERR_HIP, "near-miss list overflow after resize");
         }
         for (uint32_t b = 0; b <= base; b++) job.total[b] += sl.h_fin[b];
         if (cnt) {
+            // the list is read after the kernel has retired (its end-of-kernel
+            // cache write-back), not merely published its count
+            HIPCHK(hipEventSynchronize(done_event(sl)));
             std::vector<uint64_t> nbuf((size_t)cnt * 2);
             std::vector<uint32_t> ubuf(cnt);
             HIPCHK(hipMemcpy(nbuf.data(), sl.det.n, (size_t)cnt * 16, hipMemcpyDeviceToHost));
@@ -659,6 +749,8 @@ int nice_fd_kernel_base(uint32_t base) { return nice::fd2_supported(base) ? 1 : 
 
 int nice_last_kernel_stats(nice_ctx *ctx, int i, nice_kernel_stats *out) {
     if (!ctx || i < 0 || i >= (int)ctx->devs.size() || !out) return fail(NICE_ERR_INVALID, "bad args");
+    int rc = resolve_stats(ctx->devs[i]);
+    if (rc) return rc;
     *out = ctx->devs[i].last;
     return NICE_OK;
 }

@@ -1,0 +1,87 @@
+"""Two ranks on the GPU (gloo collectives, both ranks on device 0): the
+strong-scaling field pipeline of bench.py end to end -- the b40 1e9 field
+split two ways (contiguous detailed shards, dealt niceonly chunks), results
+exchanged and compared with the committed oracle fixtures on every rank; and
+the massive field's niceonly dealt over the two ranks, whose candidate and
+range totals must equal the oracle fixture's.  (RCCL needs one GPU per rank;
+gloo exercises the same code path on a one-GPU box.)"""
+import json
+import os
+import socket
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import nice_amd as N
+    from nice_amd import dist as D
+    out = {}
+    ctx = N.GpuContext(0)
+    try:
+        s = N.get_base_range_u128(40).range_start
+        f = N.FieldSize(s, s + 10 ** 9)
+        pipe = D.FieldPipeline(ctx, ctx, dist)
+        got = [pipe.step(f, 40) for _ in range(3)]
+        got = [g for g in got if g is not None] + pipe.drain()
+        out["fields"] = [([(d.num_uniques, d.count) for d in det.distribution],
+                          [(n.number, n.num_uniques) for n in det.nice_numbers],
+                          [str(n.number) for n in nic.nice_numbers], st.candidates, st.ranges)
+                         for _, det, nic, st in got]
+        with open(os.path.join(ROOT, "tests", "golden", "massive_b50.json")) as fh:
+            m = json.load(fh)
+        lst, st = ctx.niceonly_raw(int(m["start"]), int(m["end"]), 50, deal_stride=world,
+                                   deal_offset=rank)
+        out["massive"] = (st.candidates, st.ranges, lst)
+    finally:
+        ctx.close()
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_two_rank_strong_pipeline_on_gpu():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    with open(os.path.join(ROOT, "tests", "golden", "oracle_fields.json")) as fh:
+        fx = json.load(fh)
+    det = next(c for c in fx["detailed"] if c["name"] == "b40_extra_large_1e9")
+    nic = next(c for c in fx["niceonly"] if c["name"] == "b40_extra_large_1e9")
+    # every rank holds the whole field's results, every field equal to the fixture
+    assert len(res[0]["fields"]) == 3 and [r[:3] for r in res[0]["fields"]] == [r[:3] for r in res[1]["fields"]]
+    for r in range(2):
+        for dist_, near, nice, _, _ in res[r]["fields"]:
+            assert dist_ == [tuple(x) for x in det["distribution"]]
+            assert near == [(int(n), u) for n, u in det["near_misses"]]
+            assert nice == nic["nice_numbers"]
+    # dealt niceonly: the two ranks' candidate counts sum to the whole field's
+    assert all(a[3] + b[3] == nic["candidates"] for a, b in zip(res[0]["fields"], res[1]["fields"]))
+    with open(os.path.join(ROOT, "tests", "golden", "massive_b50.json")) as fh:
+        m = json.load(fh)
+    c = res[0]["massive"][0] + res[1]["massive"][0]
+    r_ = res[0]["massive"][1] + res[1]["massive"][1]
+    assert (c, r_) == (sum(w["candidates"] for w in m["windows"]), sum(w["ranges"] for w in m["windows"]))
+    assert res[0]["massive"][2] == [] and res[1]["massive"][2] == []
