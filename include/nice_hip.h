@@ -130,6 +130,30 @@ int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t st
 int nice_validate_detailed(uint32_t base, uint64_t size_lo, uint64_t size_hi, const uint64_t *hist,
                            const nice_number *list, size_t n);
 
+/* The reference's CPU API on the host cores, for callers without a GPU and
+ * the reference client's CPU mode (cpu_path.cpp).  No device is touched, and
+ * the GPU entry points above never fall back to these.
+ *
+ * process_range_detailed (common/src/client_process.rs:150-191): the
+ * histogram of unique-digit counts (base+1 bins) and the numbers above the
+ * near-miss cutoff, ascending -- same outputs as nice_process_range_detailed.
+ *
+ * process_range_niceonly (client_process.rs:439-465): get_valid_ranges over
+ * the whole range (msd_prefix_filter.rs:665-674, floor 250), then every
+ * candidate of the (b-1) * b^k stride table (stride_filter.rs:139-155; k =
+ * stride_k, 0 -> 2) tested with get_is_nice; the nice numbers, ascending.
+ *
+ * threads: host threads (< 1 -> 1, the reference's single-threaded call);
+ * the range (detailed) or the surviving MSD ranges (niceonly) are split
+ * into contiguous pieces.  Errors: NICE_ERR_INVALID (base outside 2..128,
+ * end < start), NICE_ERR_CAPACITY (*n_out = the required capacity). */
+int nice_cpu_process_range_detailed(uint64_t start_lo, uint64_t start_hi, uint64_t end_lo,
+                                    uint64_t end_hi, uint32_t base, int32_t threads,
+                                    uint64_t *hist, nice_number *out, size_t cap, size_t *n_out);
+int nice_cpu_process_range_niceonly(uint64_t start_lo, uint64_t start_hi, uint64_t end_lo,
+                                    uint64_t end_hi, uint32_t base, uint32_t stride_k,
+                                    int32_t threads, nice_number *out, size_t cap, size_t *n_out);
+
 /* Asynchronous fields.  *_submit enqueues a field on the context's devices
  * and returns at once with a ticket; *_collect waits for that field and
  * returns exactly what the synchronous call would (the synchronous entry

@@ -10,7 +10,8 @@ from .api import (CLIENT_VERSION, GPU_BATCH_SIZE, PROCESSING_CHUNK_SIZE, BothMod
                   get_valid_ranges, gpu_supports_base, has_duplicate_msd_prefix,
                   process_detailed_gpu, process_niceonly_gpu, process_range_detailed,
                   process_range_detailed_gpu, process_range_niceonly,
-                  process_range_niceonly_gpu)
+                  process_range_niceonly_gpu, process_range_detailed_cpu,
+                  process_range_niceonly_cpu)
 from .benchmark import BenchmarkMode, get_benchmark_field  # noqa: F401
 from .types import (DataToClient, DataToServer, FieldResults, FieldSize,  # noqa: F401
                     NiceNumberSimple, SearchMode, UniquesDistributionSimple)

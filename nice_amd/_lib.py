@@ -30,6 +30,7 @@ EXPORTS = (
     "nice_debug_is_nice", "nice_check_is_nice_inrange", "nice_check_msd_skippable_inrange",
     "nice_fd_segment_cuts", "nice_validate_detailed", "nice_detailed_submit",
     "nice_detailed_collect", "nice_niceonly_submit", "nice_niceonly_collect",
+    "nice_cpu_process_range_detailed", "nice_cpu_process_range_niceonly",
 )
 
 
@@ -124,6 +125,8 @@ def lib():
         "nice_niceonly_submit": ([vp, u64, u64, u64, u64, u32, ctypes.POINTER(nice_niceonly_opts),
                                   ctypes.POINTER(i32)], i32),
         "nice_niceonly_collect": ([vp, i32, PN, sz, PSZ, ctypes.POINTER(nice_niceonly_stats)], i32),
+        "nice_cpu_process_range_detailed": ([u64, u64, u64, u64, u32, i32, P64, PN, sz, PSZ], i32),
+        "nice_cpu_process_range_niceonly": ([u64, u64, u64, u64, u32, u32, i32, PN, sz, PSZ], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -415,3 +415,49 @@ def process_range_niceonly(range_: FieldSize, base: int,
     size = range_.range_size
     return process_range_niceonly_gpu(default_context(), range_, base, stride_k=k,
                                       chunk_size=min(size, (1 << 64) - 1))
+
+
+def _cpu_out(cap: int):
+    return (_lib.nice_number * max(cap, 1))()
+
+
+def process_range_detailed_cpu(range_: FieldSize, base: int, threads: int = 1) -> FieldResults:
+    """process_range_detailed (client_process.rs:150-191) on the host cores
+    (nice_cpu_process_range_detailed): no device, for callers without a GPU.
+    threads = 1 is the reference's single-threaded call."""
+    hist = (ctypes.c_uint64 * (base + 1))()
+    cap = 1024
+    while True:
+        out, n = _cpu_out(cap), ctypes.c_size_t()
+        rc = lib().nice_cpu_process_range_detailed(*_split(range_.range_start), *_split(range_.range_end),
+                                                    base, threads, hist, out, cap, n)
+        if rc == _lib.NICE_ERR_CAPACITY:
+            cap = n.value
+            continue
+        check(rc)
+        break
+    return FieldResults(
+        distribution=[UniquesDistributionSimple(i, hist[i]) for i in range(1, base + 1)],
+        nice_numbers=[NiceNumberSimple(out[i].number_lo | (out[i].number_hi << 64), out[i].num_uniques)
+                      for i in range(n.value)])
+
+
+def process_range_niceonly_cpu(range_: FieldSize, base: int,
+                               stride_table: Optional[StrideTable] = None,
+                               threads: int = 1) -> FieldResults:
+    """process_range_niceonly (client_process.rs:439-465) on the host cores
+    (nice_cpu_process_range_niceonly): MSD floor 250 over the whole range,
+    stride table k from `stride_table` (default 2)."""
+    k = stride_table.k if stride_table is not None else 2
+    cap = 256
+    while True:
+        out, n = _cpu_out(cap), ctypes.c_size_t()
+        rc = lib().nice_cpu_process_range_niceonly(*_split(range_.range_start), *_split(range_.range_end),
+                                                    base, k, threads, out, cap, n)
+        if rc == _lib.NICE_ERR_CAPACITY:
+            cap = n.value
+            continue
+        check(rc)
+        break
+    return FieldResults(distribution=[], nice_numbers=[
+        NiceNumberSimple(out[i].number_lo | (out[i].number_hi << 64), base) for i in range(n.value)])

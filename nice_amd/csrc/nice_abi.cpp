@@ -688,6 +688,11 @@ int detailed_collect(nice_ctx *ctx, int t, uint64_t *hist, nice_number *out, siz
 
 }  // namespace
 
+// The CPU path (cpu_path.cpp) reports through the same thread-local message.
+namespace nice {
+void set_last_error(const char *msg) { g_err = msg; }
+}  // namespace nice
+
 extern "C" {
 
 const char *nice_last_error(void) { return g_err.c_str(); }
