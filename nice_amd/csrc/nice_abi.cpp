@@ -1041,6 +1041,9 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
         // (every split child holds >= floor numbers); size batches for 2^24.
         const uint64_t fl = std::min<uint64_t>(floor_size, 1ull << 30);
         uint64_t cpb = std::max<uint64_t>(1, (fl << 24) / cnk);
+#ifdef NICE_PROBES
+        if (getenv("NICE_MSD_CPB")) cpb = std::max<uint64_t>(1, strtoull(getenv("NICE_MSD_CPB"), nullptr, 10));
+#endif
         cpb = std::min(cpb, mine);
         const uint64_t batch_n = cpb * cnk;
         uint64_t per = std::min<uint64_t>(batch_n / fl + cpb, cpb << 22) + 64;
@@ -1049,7 +1052,12 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
         const uint64_t leaf_cap = std::min<uint64_t>(per + (batch_n / nice::kLeafPiece) + 64, 0xffffffffull);
         // Chunks whose recursion fits a workgroup run fused: one launch per
         // batch, one workgroup per chunk (grid-strided), no level queues.
+#ifdef NICE_PROBES
+        const uint32_t fcap = getenv("NICE_MSD_FCAP") && cnk <= 0xffffffffull
+                                  ? (uint32_t)atoi(getenv("NICE_MSD_FCAP")) : nice::msd_fused_cap(cnk, floor_size);
+#else
         const uint32_t fcap = nice::msd_fused_cap(cnk, floor_size);
+#endif
         const uint64_t nbatches = nbatches_of(mine, cpb);
         for (size_t i = 0; i < ctx->devs.size(); i++) {
             Device &d = ctx->devs[i];

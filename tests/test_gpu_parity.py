@@ -506,6 +506,21 @@ def test_field_pipeline_on_gpu():
         b.close()
 
 
+def test_fd_bases_whole_fields_1e9(ctx):
+    """The CLI hi-base field (b80 1e9, benchmark.rs:63) and the live bases
+    52 / 53 / 54 (1e9 from each range start): the whole field's distribution
+    and near-miss list against the oracle fixture (gen_fd_bases_fixtures.py)."""
+    p = os.path.join(ROOT, "tests", "golden", "fd_bases_1e9.json")
+    with open(p) as f:
+        fx = json.load(f)
+    assert [c["base"] for c in fx["detailed"]] == [80, 52, 53, 54]
+    for c in fx["detailed"]:
+        hist, lst = ctx.detailed_raw(int(c["start"]), int(c["end"]), c["base"])
+        assert _dist(hist) == [tuple(x) for x in c["distribution"]], c["name"]
+        assert lst == [(int(n), u) for n, u in c["near_misses"]], c["name"]
+        assert ctx.kernel_stats().fd_kernel == 1
+
+
 # --- massive config (benchmark.rs:62): b50 [start, +1e13), niceonly ----------
 def _massive():
     p = os.path.join(ROOT, "tests", "golden", "massive_b50.json")

@@ -175,3 +175,30 @@ def test_massive_fixture_consistent():
     x = w[72]
     r, c, rg = O.process_field_niceonly_ex(int(x["start"]), int(x["end"]), 50, 8, chunk=10 ** 8)
     assert (c, rg) == (x["candidates"], x["ranges"]) == (86, x["ranges"]) and r.nice_numbers == []
+
+
+def test_fd_bases_fixture_consistent():
+    """tests/golden/fd_bases_1e9.json: each field is 1e9 from its base's range
+    start, the distribution sums to 1e9, and the near-miss list matches the
+    bins above the cutoff; a 1e5 prefix of the b80 field re-checked against
+    the oracle's distribution shape (the same n have at most the whole
+    field's counts)."""
+    import json
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fd_bases_1e9.json")
+    fx = json.load(open(p))
+    for c in fx["detailed"]:
+        b = c["base"]
+        s = int(c["start"])
+        assert s == O.base_range(b)[0] and int(c["end"]) == s + 10 ** 9
+        hist = dict((u, n) for u, n in c["distribution"])
+        assert [u for u, _ in c["distribution"]] == list(range(1, b + 1))
+        assert sum(hist.values()) == 10 ** 9
+        cut = O.near_miss_cutoff(b)
+        assert sum(n for u, n in hist.items() if u > cut) == len(c["near_misses"])
+        assert all(u > cut for _, u in c["near_misses"])
+    b80 = fx["detailed"][0]
+    s = int(b80["start"])
+    pre = O.process_range_detailed(s, s + 10 ** 5, 80)
+    full = dict((u, n) for u, n in b80["distribution"])
+    assert all(n <= full[u] for u, n in pre.distribution)
