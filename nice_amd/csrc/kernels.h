@@ -99,10 +99,10 @@ hipError_t launch_niceonly(const NiceonlyLaunch &p, int num_cus, hipStream_t s);
 // Device MSD filter (msd_prefix_filter.rs:583-658 as a level-synchronous BFS):
 // one lane per node; leaves (already in stride-index form) are appended to
 // `leaves`.  Nodes: {start lo, hi, size, depth}.
+// A level-queue node: numbers [start + off, start + off + size) of the field
+// (off < field size < 2^63; the level is the queue's).
 struct MsdNode {
-    uint64_t lo, hi;
-    uint64_t size;
-    uint32_t depth, pad;
+    uint64_t off, size;
 };
 struct MsdLaunch {
     // The batch's level-0 nodes are the field's chunks c_j = deal_offset +

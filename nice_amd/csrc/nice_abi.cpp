@@ -1038,16 +1038,21 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
         if ((e - s) >> 63) return fail(NICE_ERR_INVALID, "device MSD: field larger than 2^63");
         const uint64_t cnk = (uint64_t)chunk;
         // Nodes per level and leaves per batch are <= batch / floor + chunks
-        // (every split child holds >= floor numbers); size batches for 2^24.
+        // (every split child holds >= floor numbers); size batches for 2^27
+        // (16-byte nodes: 2 x 2 GB of level queues and 3 GB of leaf records at
+        // most, allocated as a field needs them).  Batches are the unit of the
+        // level launches, so larger ones amortise their fixed cost: the massive
+        // field (chunk 1e8) took 0.365 s at 41 chunks per batch (2^24), 0.20 s
+        // at 164, 0.17 s at 328 (profiles/r02/massive_batch_sweep.log).
         const uint64_t fl = std::min<uint64_t>(floor_size, 1ull << 30);
-        uint64_t cpb = std::max<uint64_t>(1, (fl << 24) / cnk);
+        uint64_t cpb = std::max<uint64_t>(1, (fl << 27) / cnk);
 #ifdef NICE_PROBES
         if (getenv("NICE_MSD_CPB")) cpb = std::max<uint64_t>(1, strtoull(getenv("NICE_MSD_CPB"), nullptr, 10));
 #endif
         cpb = std::min(cpb, mine);
         const uint64_t batch_n = cpb * cnk;
         uint64_t per = std::min<uint64_t>(batch_n / fl + cpb, cpb << 22) + 64;
-        per = std::min<uint64_t>(per, 1ull << 26);
+        per = std::min<uint64_t>(per, 1ull << 28);  // (the bound above stays below this)
         // leaf records: one per range plus one per kLeafPiece candidates
         const uint64_t leaf_cap = std::min<uint64_t>(per + (batch_n / nice::kLeafPiece) + 64, 0xffffffffull);
         // Chunks whose recursion fits a workgroup run fused: one launch per

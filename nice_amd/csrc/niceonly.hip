@@ -314,7 +314,7 @@ __global__ void msd_init_kernel(MsdLaunch p) {
         const u64 rem_lo = p.end_lo - lo;
         const u64 rem_hi = p.end_hi - hi - (p.end_lo < lo ? 1 : 0);
         const u64 size = rem_hi || rem_lo > p.chunk ? p.chunk : rem_lo;
-        p.q[0][i] = MsdNode{lo, hi, size, 0u, 0u};
+        p.q[0][i] = MsdNode{c * p.chunk, size};
     }
     // counters: [0] level-0 size, [1..24] per batch, [25..31] sticky over the
     // field (zeroed with the first batch, as is the field's nice count)
@@ -461,12 +461,14 @@ msd_level_kernel(MsdLaunch p, u32 level, G g) {
     for (u32 b0 = blockIdx.x * blockDim.x; b0 < n_in; b0 += stride) {
         const u32 i = b0 + threadIdx.x;
         u32 act = 0;  // 0 drop / idle, 1 leaf, 2 split
-        MsdNode nd{0, 0, 0, 0, 0};
+        MsdNode nd{0, 0};
+        u64 lo = p.start_lo, hi = p.start_hi;
         if (i < n_in) {
             nd = qin[i];
-            act = classify_node(p, level, nd.lo, nd.hi, nd.size, g);
+            add_u128(lo, hi, nd.off);
+            act = classify_node(p, level, lo, hi, nd.size, g);
         }
-        append_leaf<MC>(p, act, nd.lo, nd.hi, nd.size, slots, n_st, c_st, s_st);
+        append_leaf<MC>(p, act, lo, hi, nd.size, slots, n_st, c_st, s_st);
         // children
         const u32 cpos = block_reserve(&p.counters[level + 1], act == 2 ? 2u : 0u, slots);
         if (act == 2) {
@@ -474,10 +476,8 @@ msd_level_kernel(MsdLaunch p, u32 level, G g) {
                 atomicOr(&p.counters[25], 1u);
             } else {
                 const u64 half = nd.size / 2;
-                u64 m_lo = nd.lo, m_hi = nd.hi;
-                add_u128(m_lo, m_hi, half);
-                qout[cpos] = MsdNode{nd.lo, nd.hi, half, level + 1, 0u};
-                qout[cpos + 1] = MsdNode{m_lo, m_hi, nd.size - half, level + 1, 0u};
+                qout[cpos] = MsdNode{nd.off, half};
+                qout[cpos + 1] = MsdNode{nd.off + half, nd.size - half};
             }
         }
     }
