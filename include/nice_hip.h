@@ -217,8 +217,11 @@ int nice_stride_table(uint32_t base, uint32_t k, uint64_t *modulus, uint32_t *re
  * kernels (radix_fast.hpp) evaluated on the host, bases 40/50/52/53/54/80 with n (and
  * [start, end)) inside the base's valid range.  is_nice: 1/0 like get_is_nice
  * (client_process.rs:222-253); msd: 1/0 like has_duplicate_msd_prefix on
- * [start, end - 1] (msd_prefix_filter.rs:382-563).  NICE_ERR_INVALID otherwise. */
+ * [start, end - 1] (msd_prefix_filter.rs:382-563); unique: the unique-digit
+ * count of n^2 and n^3 by the same limb path (get_num_unique_digits,
+ * client_process.rs:47-143).  NICE_ERR_INVALID otherwise. */
 int nice_check_is_nice_inrange(uint32_t base, uint64_t n_lo, uint64_t n_hi);
+int nice_check_unique_inrange(uint32_t base, uint64_t n_lo, uint64_t n_hi);
 int nice_check_msd_skippable_inrange(uint32_t base, uint64_t start_lo, uint64_t start_hi,
                                      uint64_t end_lo, uint64_t end_hi);
 /* Limb-count cuts of the production FD kernel (fd2_detailed.hip): the n at
@@ -231,6 +234,11 @@ int nice_debug_unique_counts(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t co
                              uint32_t base, uint32_t *out);
 int nice_debug_is_nice(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t count, uint32_t base,
                        uint32_t *out);
+/* The niceonly kernel's in-range limb path (bases 40/50/52/53/54/80, every n
+ * inside the base's valid range, else NICE_ERR_INVALID): the unique-digit
+ * count its niceness test compares with the base. */
+int nice_debug_unique_fast(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t count, uint32_t base,
+                           uint32_t *out);
 
 #ifdef __cplusplus
 }

@@ -27,7 +27,7 @@ EXPORTS = (
     "nice_near_miss_cutoff", "nice_gpu_batch_size", "nice_processing_chunk_size",
     "nice_gpu_supports_base", "nice_fd_kernel_base", "nice_msd_valid_ranges",
     "nice_msd_skippable", "nice_stride_table", "nice_debug_unique_counts",
-    "nice_debug_is_nice", "nice_check_is_nice_inrange", "nice_check_msd_skippable_inrange",
+    "nice_debug_is_nice", "nice_debug_unique_fast", "nice_check_is_nice_inrange", "nice_check_unique_inrange", "nice_check_msd_skippable_inrange",
     "nice_fd_segment_cuts", "nice_validate_detailed", "nice_detailed_submit",
     "nice_detailed_collect", "nice_niceonly_submit", "nice_niceonly_collect",
     "nice_cpu_process_range_detailed", "nice_cpu_process_range_niceonly",
@@ -116,7 +116,9 @@ def lib():
         "nice_stride_table": ([u32, u32, P64, P32, sz, PSZ], i32),
         "nice_debug_unique_counts": ([vp, P64, u32, u32, P32], i32),
         "nice_debug_is_nice": ([vp, P64, u32, u32, P32], i32),
+        "nice_debug_unique_fast": ([vp, P64, u32, u32, P32], i32),
         "nice_check_is_nice_inrange": ([u32, u64, u64], i32),
+        "nice_check_unique_inrange": ([u32, u64, u64], i32),
         "nice_check_msd_skippable_inrange": ([u32, u64, u64, u64, u64], i32),
         "nice_fd_segment_cuts": ([u32, P64, sz, PSZ], i32),
         "nice_validate_detailed": ([u32, u64, u64, P64, PN, sz], i32),

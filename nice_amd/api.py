@@ -280,6 +280,16 @@ class GpuContext:
         check(lib().nice_debug_unique_counts(self._h, arr, len(ns), base, out))
         return list(out[: len(ns)])
 
+    def debug_unique_fast(self, ns: Sequence[int], base: int) -> List[int]:
+        """Unique-digit counts by the niceonly kernel's in-range limb path
+        (radix_fast.hpp); every n must lie in the base's valid range."""
+        arr = (ctypes.c_uint64 * (2 * max(len(ns), 1)))()
+        for i, n in enumerate(ns):
+            arr[2 * i], arr[2 * i + 1] = _split(n)
+        out = (ctypes.c_uint32 * max(len(ns), 1))()
+        check(lib().nice_debug_unique_fast(self._h, arr, len(ns), base, out))
+        return list(out[: len(ns)])
+
     def debug_is_nice(self, ns: Sequence[int], base: int) -> List[bool]:
         arr = (ctypes.c_uint64 * (2 * max(len(ns), 1)))()
         for i, n in enumerate(ns):

@@ -156,5 +156,9 @@ hipError_t launch_unique_counts(const uint64_t *n_pairs, uint32_t count, uint32_
                                 uint32_t *out, hipStream_t s);
 hipError_t launch_is_nice(const uint64_t *n_pairs, uint32_t count, uint32_t base,
                           uint32_t *out, hipStream_t s);
+// In-range n of a niceonly fast base (40/50/52/53/54/80): the unique-digit
+// count by niceonly_kernel's limb path (radix_fast.hpp unique_fast).
+hipError_t launch_unique_fast(const uint64_t *n_pairs, uint32_t count, uint32_t base,
+                              uint32_t *out, hipStream_t s);
 
 }  // namespace nice

@@ -853,6 +853,31 @@ static bool nice_fast_base(uint32_t base) {
     }
 }
 
+int nice_debug_unique_fast(nice_ctx *ctx, const uint64_t *n_pairs, uint32_t count, uint32_t base,
+                           uint32_t *out) {
+    u128 rs, re;
+    if (!ctx || !nice_fast_base(base) || nice::base_range_cached(base, rs, re) != 1)
+        return fail(NICE_ERR_INVALID, "base without a niceonly fast path");
+    for (uint32_t i = 0; i < count; i++) {
+        const u128 n = mk(n_pairs[2 * i], n_pairs[2 * i + 1]);
+        if (n < rs || n >= re) return fail(NICE_ERR_INVALID, "n outside the base's valid range");
+    }
+    if (count == 0) return NICE_OK;
+    Device &d = ctx->devs[0];
+    HIPCHK(hipSetDevice(d.id));
+    uint64_t *dn;
+    uint32_t *du;
+    HIPCHK(hipMalloc(&dn, (size_t)count * 16));
+    HIPCHK(hipMalloc(&du, (size_t)count * 4));
+    HIPCHK(hipMemcpy(dn, n_pairs, (size_t)count * 16, hipMemcpyHostToDevice));
+    HIPCHK(nice::launch_unique_fast(dn, count, base, du, d.slot[0].stream));
+    HIPCHK(hipStreamSynchronize(d.slot[0].stream));
+    HIPCHK(hipMemcpy(out, du, (size_t)count * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipFree(dn));
+    HIPCHK(hipFree(du));
+    return NICE_OK;
+}
+
 int nice_check_is_nice_inrange(uint32_t base, uint64_t lo, uint64_t hi) {
     u128 rs, re;
     const u128 n = mk(lo, hi);
@@ -860,6 +885,19 @@ int nice_check_is_nice_inrange(uint32_t base, uint64_t lo, uint64_t hi) {
         return fail(NICE_ERR_INVALID, "n outside the base's valid range (or base not 40/50/80)");
     switch (base) {
 #define X(b) case b: return nice::is_nice_fast<b>(lo, hi) ? 1 : 0;
+        NICE_FAST_BASES(X)
+#undef X
+    default: return NICE_ERR_INVALID;
+    }
+}
+
+int nice_check_unique_inrange(uint32_t base, uint64_t lo, uint64_t hi) {
+    u128 rs, re;
+    const u128 n = mk(lo, hi);
+    if (!nice_fast_base(base) || nice::base_range_cached(base, rs, re) != 1 || n < rs || n >= re)
+        return fail(NICE_ERR_INVALID, "n outside the base's valid range (or base not 40/50/52/53/54/80)");
+    switch (base) {
+#define X(b) case b: return (int)nice::unique_fast<b>(lo, hi);
         NICE_FAST_BASES(X)
 #undef X
     default: return NICE_ERR_INVALID;

@@ -38,6 +38,44 @@ struct IsConst<ConstBase<B>> {
 // ---------------------------------------------------------------------------
 // Candidate check kernel
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ u32 lane_rank(u64 mask) {
+    return __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u));
+}
+
+__device__ __forceinline__ void emit_nice(const NiceonlyLaunch &p, u64 n_lo, u64 n_hi) {
+    const u32 pos = atomicAdd(p.out.count, 1u);
+    if (pos < p.out.cap) {
+        p.out.n[2 * (u64)pos] = n_lo;
+        p.out.n[2 * (u64)pos + 1] = n_hi;
+    }
+}
+
+// Square-survivor ring per wave (entries; a power of two >= 128: a round adds
+// at most 64 to fewer than 64 queued).
+constexpr u32 kCubeQ = 128;
+
+// The full niceness test on `cnt` <= 64 queued candidates, one per lane.  At
+// the MSD floor about one stride candidate in ~20 has a repeat-free square
+// (the MSD filter already vetted the leading digits), yet nearly every round of
+// 64 holds one: testing the cube in place ran the 220-instruction cube for
+// almost every wave and round.  Queued, it runs once per 64 survivors.
+template <int B>
+__device__ __forceinline__ void cube_pass(const NiceonlyLaunch &p, const ulonglong2 *q, u32 head, u32 cnt,
+                                          u32 lane) {
+    // the queue was written by other lanes of this wave: order the LDS
+    // accesses (one wave, so no workgroup barrier)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < cnt) {
+        const ulonglong2 e = q[(head + lane) & (kCubeQ - 1)];
+        if (is_nice_fast<B>(e.x, e.y)) emit_nice(p, e.x, e.y);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <class G>
 __global__ void __launch_bounds__(256)
 niceonly_kernel(NiceonlyLaunch p, G g) {
@@ -45,6 +83,17 @@ niceonly_kernel(NiceonlyLaunch p, G g) {
     const u32 gwave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const u32 nwaves = (gridDim.x * blockDim.x) >> 6;
     const u32 n_leaves = p.n_leaves_dev ? min(*p.n_leaves_dev, p.n_leaves) : p.n_leaves;
+    // gi / R by one 32x32->64 multiply and a shift: gi = g0 + j < R + 2^28 <
+    // 2^29 and m = floor(2^s / R) + 1 with s = 30 + ceil(log2 R) keep the error
+    // below 2^-(L+1) <= 1/(2R), so the quotient is exact (m < 2^31 + 1).
+    const u32 r_log = 32 - __clz(p.R - 1);
+    const u64 r_magic = (1ull << (30 + r_log)) / p.R + 1;
+    const u32 r_shift = 30 + r_log;
+    // In-range fast bases: per-wave ring of the candidates whose square is
+    // repeat-free (see cube_pass); head / tail are wave-uniform.
+    __shared__ ulonglong2 cq[4][IsConst<G>::value ? kCubeQ : 1];
+    const u32 wv = threadIdx.x >> 6;
+    u32 q_head = 0, q_tail = 0;
     // LPW leaves per wave (lanes >= LPW carry count 0): at the CPU path's
     // floor a leaf holds ~40 candidates, so 8 leaves keep a wave ~5 rounds
     // deep and spread a 35k-leaf field over ~4400 waves instead of ~550.
@@ -74,27 +123,39 @@ niceonly_kernel(NiceonlyLaunch p, G g) {
             const u32 j = k - __shfl(excl, lo);
             const u32 g0 = __shfl(lf.g0, lo);
             const u64 b0lo = __shfl(lf.b0_lo, lo), b0hi = __shfl(lf.b0_hi, lo);
+            u64 n_lo = 0, n_hi = 0;
             if (k < total) {
                 const u32 gi = g0 + j;
-                const u32 cyc = gi / p.R;
+                const u32 cyc = (u32)(((u64)gi * r_magic) >> r_shift);
                 const u32 idx = gi - cyc * p.R;
-                u64 n_lo = b0lo, n_hi = b0hi;
+                n_lo = b0lo;
+                n_hi = b0hi;
                 add_u128(n_lo, n_hi, (u64)cyc * p.M + p.residues[idx]);
-                bool nice;
-                if constexpr (IsConst<G>::value) {
-                    nice = p.in_range ? is_nice_fast<IsConst<G>::base>(n_lo, n_hi) : is_nice_dev(n_lo, n_hi, g);
-                } else {
-                    nice = is_nice_dev(n_lo, n_hi, g);
-                }
-                if (nice) {
-                    u32 pos = atomicAdd(p.out.count, 1u);
-                    if (pos < p.out.cap) {
-                        p.out.n[2 * (u64)pos] = n_lo;
-                        p.out.n[2 * (u64)pos + 1] = n_hi;
+            }
+            if constexpr (IsConst<G>::value) {
+                if (p.in_range) {  // wave-uniform
+                    // n^2 first; the few survivors queue for a full-wave cube pass
+                    const bool sq = k < total && square_ok<IsConst<G>::base>(n_lo, n_hi);
+                    const u64 bal = __ballot(sq);
+                    if (bal) {
+                        if (sq) {
+                            const u32 slot = (q_tail + lane_rank(bal)) & (kCubeQ - 1);
+                            cq[wv][slot] = make_ulonglong2(n_lo, n_hi);
+                        }
+                        q_tail += (u32)__popcll(bal);
+                        if (q_tail - q_head >= 64) {
+                            cube_pass<IsConst<G>::base>(p, cq[wv], q_head, 64, lane);
+                            q_head += 64;
+                        }
                     }
+                    continue;
                 }
             }
+            if (k < total && is_nice_dev(n_lo, n_hi, g)) emit_nice(p, n_lo, n_hi);
         }
+    }
+    if constexpr (IsConst<G>::value) {
+        if (q_tail != q_head) cube_pass<IsConst<G>::base>(p, cq[wv], q_head, q_tail - q_head, lane);
     }
     if (p.fin.done) {
         // last workgroup: the field's results to mapped host memory (the
@@ -277,9 +338,6 @@ __device__ __forceinline__ LeafDesc leaf_desc(u64 a_lo, u64 a_hi, u64 size, cons
 }
 
 // Wave-level helpers (every lane of the wave calls them together).
-__device__ __forceinline__ u32 lane_rank(u64 mask) {
-    return __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u));
-}
 __device__ __forceinline__ u64 wave_sum(u64 v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
@@ -662,6 +720,28 @@ hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s, Chu
         NICE_NICEONLY_BASES(X)
 #undef X
     default: return launch_msd(p, make_generic(p.base), num_cus, s);
+    }
+}
+
+// Diagnostics: the in-range fast path's unique-digit count (the popcount that
+// niceonly_kernel's in-range test compares with the base), per n.
+template <int B>
+__global__ void unique_fast_kernel(const u64 *n_pairs, u32 count, u32 *out) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) out[i] = unique_fast<B>(n_pairs[2 * i], n_pairs[2 * i + 1]);
+}
+
+hipError_t launch_unique_fast(const uint64_t *n_pairs, uint32_t count, uint32_t base, uint32_t *out,
+                              hipStream_t s) {
+    switch (base) {
+#define X(b)                                                                                     \
+    case b:                                                                                       \
+        hipLaunchKernelGGL(unique_fast_kernel<b>, dim3((count + 255) / 256), dim3(256), 0, s, n_pairs, \
+                           count, out);                                                           \
+        return hipGetLastError();
+        NICE_NICEONLY_BASES(X)
+#undef X
+    default: return hipErrorInvalidValue;
     }
 }
 

@@ -1,4 +1,4 @@
-// radix_fast.hpp -- in-range fast paths for the niceonly kernels (b40/50/80).
+// radix_fast.hpp -- in-range fast paths for the niceonly kernels (b40/50/52/53/54/80).
 //
 // Inside a base's valid range n^2 and n^3 have exactly D2 and D3 base-b digits
 // (base_range.rs:14-32), so both fit fixed radix-B = b^2 limb arrays sized at
@@ -7,9 +7,9 @@
 // path's chunked long division of 8- and 12-word numbers by b^E: the digit
 // pairs fall out of the limbs, and the dependent chains are a few steps long
 // instead of hundreds.  Used by
-//   * is_nice_fast      == get_is_nice (client_process.rs:222-253): n^2 then
-//                          n^3, least significant digit first, stop at the
-//                          first repeat;
+//   * is_nice_fast      == get_is_nice (client_process.rs:222-253): with
+//                          exactly b digits in n^2 and n^3, "no digit
+//                          repeats" is "the digit union has b members";
 //   * msd_skippable_fast == has_duplicate_msd_prefix (msd_prefix_filter.rs:
 //                          382-563) incl. Filter C, for [first, last] in range.
 // Both agree bit-for-bit with the generic device functions (nice_device.hpp,
@@ -131,20 +131,64 @@ __host__ __device__ __forceinline__ void cube_limbs(const u32 (&S)[Radix<BASE>::
     }
 }
 
-// Digits of limb array A (D digits, LSD first) into m; false at the first repeat.
-template <int BASE, int N>
-__host__ __device__ __forceinline__ bool scan_limbs(const u32 (&A)[N], int D, u32 (&m)[Radix<BASE>::MW]) {
-#pragma unroll
-    for (int t = 0; t < N; t++) {
-        const u32 d1 = A[t] / BASE, d0 = A[t] - d1 * BASE;
-        if (mset(m, d0)) return false;
-        if (2 * t + 1 < D && mset(m, d1)) return false;
+__host__ __device__ __forceinline__ u32 popc32(u32 x) { return (u32)__builtin_popcount(x); }
+
+// Digit bits of a radix-B limb v (two base-b digits, or one when `two` is
+// false: the top limb of an odd digit count) OR-ed into m, by VALU: the high
+// digit by one multiply-high, the low one by a multiply-subtract, each bit by
+// a 64-bit shift (digits >= 64 go to word 2 at MW = 3).  No repeat test: the
+// caller counts the union.
+template <int BASE>
+__host__ __device__ __forceinline__ void or_limb(u32 v, bool two, u32 (&m)[Radix<BASE>::MW]) {
+    constexpr int MW = Radix<BASE>::MW;
+    const u32 d1 = v / BASE, d0 = v - d1 * BASE;
+    if constexpr (MW == 2) {
+        const u64 bits = (1ull << d0) | (two ? 1ull << d1 : 0ull);
+        m[0] |= (u32)bits;
+        m[1] |= (u32)(bits >> 32);
+    } else {
+        static_assert(MW == 3, "in-range fast bases are 33..96");
+        const u64 b0 = d0 < 64 ? 1ull << (d0 & 63) : 0ull, b1 = two && d1 < 64 ? 1ull << (d1 & 63) : 0ull;
+        m[0] |= (u32)(b0 | b1);
+        m[1] |= (u32)((b0 | b1) >> 32);
+        m[2] |= (d0 >= 64 ? 1u << (d0 & 31) : 0u) | (two && d1 >= 64 ? 1u << (d1 & 31) : 0u);
     }
-    return true;
 }
 
+template <int BASE, int N>
+__host__ __device__ __forceinline__ u32 limbs_popcount(const u32 (&A)[N], int D, u32 (&m)[Radix<BASE>::MW]) {
+#pragma unroll
+    for (int t = 0; t < N; t++) or_limb<BASE>(A[t], 2 * t + 1 < D, m);
+    u32 c = 0;
+#pragma unroll
+    for (int w = 0; w < Radix<BASE>::MW; w++) c += popc32(m[w]);
+    return c;
+}
+
+// get_is_nice (client_process.rs:222-253) for in-range n.  Inside the valid
+// range n^2 and n^3 have exactly D2 + D3 = b digits, so "no digit repeats"
+// (the reference's early-exit scan, n^2 then n^3) is "the union of their
+// digits has b members": no per-digit test or branch, one popcount after n^2
+// (a repeat there ends it; the cube is multiplied out only for the ~1-2 % of
+// stride candidates whose square is repeat-free) and one after n^3.
 template <int BASE>
-__host__ __device__ __forceinline__ bool is_nice_fast(u64 lo, u64 hi) {
+__host__ __device__ __forceinline__ bool is_nice_limbs(const u32 (&X)[Radix<BASE>::NX]) {
+    using R = Radix<BASE>;
+    u32 S[R::NS];
+    square_limbs<BASE>(X, S);
+    u32 m[R::MW];
+#pragma unroll
+    for (int w = 0; w < R::MW; w++) m[w] = 0;
+    if (limbs_popcount<BASE>(S, R::D2, m) != (u32)R::D2) return false;
+    u32 C[R::NC];
+    cube_limbs<BASE>(S, X, C);
+    return limbs_popcount<BASE>(C, R::D3, m) == (u32)BASE;
+}
+
+// First half of is_nice_limbs: n^2 repeat-free (the stride candidates that
+// pass go on to the cube; niceonly_kernel batches them, see there).
+template <int BASE>
+__host__ __device__ __forceinline__ bool square_ok(u64 lo, u64 hi) {
     using R = Radix<BASE>;
     u32 X[R::NX], S[R::NS];
     to_limbs<BASE>(lo, hi, X);
@@ -152,10 +196,30 @@ __host__ __device__ __forceinline__ bool is_nice_fast(u64 lo, u64 hi) {
     u32 m[R::MW];
 #pragma unroll
     for (int w = 0; w < R::MW; w++) m[w] = 0;
-    if (!scan_limbs<BASE>(S, R::D2, m)) return false;
-    u32 C[R::NC];
+    return limbs_popcount<BASE>(S, R::D2, m) == (u32)R::D2;
+}
+
+template <int BASE>
+__host__ __device__ __forceinline__ bool is_nice_fast(u64 lo, u64 hi) {
+    u32 X[Radix<BASE>::NX];
+    to_limbs<BASE>(lo, hi, X);
+    return is_nice_limbs<BASE>(X);
+}
+
+// Unique-digit count of in-range n by the same limb path (test hook: checks
+// every digit bit the niceness test relies on against the oracle).
+template <int BASE>
+__host__ __device__ __forceinline__ u32 unique_fast(u64 lo, u64 hi) {
+    using R = Radix<BASE>;
+    u32 X[R::NX], S[R::NS], C[R::NC];
+    to_limbs<BASE>(lo, hi, X);
+    square_limbs<BASE>(X, S);
     cube_limbs<BASE>(S, X, C);
-    return scan_limbs<BASE>(C, R::D3, m);
+    u32 m[R::MW];
+#pragma unroll
+    for (int w = 0; w < R::MW; w++) m[w] = 0;
+    limbs_popcount<BASE>(S, R::D2, m);
+    return limbs_popcount<BASE>(C, R::D3, m);
 }
 
 // Common most-significant prefix of two D-digit limb arrays: its digit mask

@@ -184,6 +184,19 @@ def test_is_nice_fast_path_matches_oracle(base):
 
 
 @pytest.mark.parametrize("base", [40, 50, 52, 53, 54, 80])
+def test_unique_fast_path_matches_oracle(base):
+    """The digit bits behind is_nice_fast's popcount test: radix_fast.hpp's
+    limb path counts the unique digits of n^2 and n^3 exactly as the oracle's
+    get_num_unique_digits, at both range ends and on random in-range n."""
+    L = _lib.lib()
+    rng = random.Random(7 * base)
+    s, e = O.base_range(base)
+    for n in [s, s + 1, e - 2, e - 1] + [rng.randrange(s, e) for _ in range(2000)]:
+        assert L.nice_check_unique_inrange(base, *_split(n)) == O.num_unique_digits(n, base), n
+    assert L.nice_check_unique_inrange(base, *_split(e)) == _lib.NICE_ERR_INVALID
+
+
+@pytest.mark.parametrize("base", [40, 50, 52, 53, 54, 80])
 def test_msd_fast_path_matches_oracle(base):
     """radix_fast.hpp's msd_skippable_fast (the device MSD filter's in-range
     check) against the oracle's has_duplicate_msd_prefix, on random ranges of

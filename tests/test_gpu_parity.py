@@ -206,6 +206,25 @@ def test_device_is_nice(ctx, golden):
     assert ctx.debug_is_nice(ns, 10) == [O.is_nice(n, 10) for n in ns]
 
 
+@pytest.mark.parametrize("base", [40, 50, 52, 53, 54, 80])
+def test_device_unique_fast_path(ctx, golden, base):
+    """The niceonly kernel's in-range test is "the digit union of n^2 and n^3
+    has b members" (radix_fast.hpp is_nice_limbs).  No nice number is known at
+    these bases, so its True branch is pinned through the count itself: the
+    device limb path's unique counts equal the oracle's on both range ends,
+    random n, and the Python-mirror samples of this base."""
+    rng = random.Random(11 * base)
+    s, e = O.base_range(base)
+    ns = [s, s + 1, e - 2, e - 1] + [rng.randrange(s, e) for _ in range(3000)]
+    want = [O.num_unique_digits(n, base) for n in ns]
+    for c in golden["python"]["samples"]:
+        if c["base"] == base:
+            ins = [(int(n), u) for n, u in zip(c["n"], c["num_uniques"]) if s <= int(n) < e]
+            ns += [n for n, _ in ins]
+            want += [u for _, u in ins]
+    assert ctx.debug_unique_fast(ns, base) == want
+
+
 # --- niceonly ---------------------------------------------------------------
 def test_niceonly_reference_vectors(ctx, golden):
     for c in golden["reference"]["niceonly"]:
