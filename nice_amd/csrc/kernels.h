@@ -150,6 +150,17 @@ uint32_t msd_fused_cap(uint64_t chunk, uint64_t floor_size);
 hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s, ChunkNode *scratch = nullptr,
                              uint32_t cap = 0, uint32_t grid = 0);
 
+// Large chunks: init + the level BFS down to `level0` (nodes <= 2^26 numbers,
+// enough roots to fill the chip), then msd_wave_kernel: the recursion below
+// level0 AND the candidate test of every leaf in one launch (`c` holds the
+// residues, output and finish; its leaf fields are unused), `grid` workgroups
+// of 4 waves, each wave with a kStackCap-node stack in `scratch`
+// (msd_wave_scratch_bytes(grid)).  Leaves of the BFS levels go to p.leaves
+// and are tested by the same launch.
+hipError_t launch_msd_wave(const MsdLaunch &p, const NiceonlyLaunch &c, uint32_t level0, void *scratch,
+                           uint32_t grid, int num_cus, hipStream_t s);
+size_t msd_wave_scratch_bytes(uint32_t grid);
+
 // Diagnostics used by the parity tests: per-n unique counts / nice flags
 // computed by the same device functions the production kernels use.
 hipError_t launch_unique_counts(const uint64_t *n_pairs, uint32_t count, uint32_t base,

@@ -116,6 +116,8 @@ struct MsdBuf {
     // queues), leaf list, counters (kernels.h).
     nice::MsdNode *q[2] = {nullptr, nullptr};
     nice::ChunkNode *scratch = nullptr;
+    void *wscratch = nullptr;  // msd_wave_kernel work stacks
+    size_t wscratch_bytes = 0;
     nice::Leaf *leaves = nullptr;
     uint32_t *counters = nullptr;  // 32 words
     uint32_t q_cap = 0, leaf_cap = 0;
@@ -251,9 +253,15 @@ int ensure_desc(LeafBuf &b, uint32_t cap) {
     return NICE_OK;
 }
 
-int ensure_msd(Slot &sl, uint32_t q_cap, uint32_t leaf_cap, uint64_t scratch_nodes) {
+int ensure_msd(Slot &sl, uint32_t q_cap, uint32_t leaf_cap, uint64_t scratch_nodes, size_t wscratch_bytes = 0) {
     MsdBuf &m = sl.msd;
     if (!m.counters) HIPCHK(hipMalloc(&m.counters, 32 * 4));
+    if (m.wscratch_bytes < wscratch_bytes) {
+        HIPCHK(hipStreamSynchronize(sl.nstream));
+        if (m.wscratch) HIPCHK(hipFree(m.wscratch));
+        HIPCHK(hipMalloc(&m.wscratch, wscratch_bytes));
+        m.wscratch_bytes = wscratch_bytes;
+    }
     if (m.scratch_nodes < scratch_nodes) {
         HIPCHK(hipStreamSynchronize(sl.nstream));
         if (m.scratch) HIPCHK(hipFree(m.scratch));
@@ -1101,13 +1109,47 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
 #else
         const uint32_t fcap = nice::msd_fused_cap(cnk, floor_size);
 #endif
+        // Chunks too large for the fused kernel: the level BFS only down to a
+        // root level `wlevel` (nodes <= 2^26 numbers, >= 8 roots per wave of
+        // the fused MSD + candidate kernel), then msd_wave_kernel.  Nothing of
+        // a batch grows with its survivors any more (leaves are tested inside
+        // the wave that finds them), so a batch is bounded only by the level
+        // queues: 2^24 nodes at the root level.  The massive field is ONE
+        // batch.
+        bool wave = !fcap;
+#ifdef NICE_PROBES
+        if (getenv("NICE_MSD_NOWAVE")) wave = false;  // A/B: the level-BFS + leaf-list path
+#endif
+        uint32_t wlevel = 0, wgrid = 0;
+        uint64_t wleaf_cap = 0;
+        if (wave) {
+            int cus = 256;
+            for (auto &d : ctx->devs) cus = std::max(cus, d.num_cus);
+            wgrid = (uint32_t)cus * 4;
+            const uint64_t target = (uint64_t)wgrid * 4 * 8;
+            uint32_t last = 0;  // first level without splits
+            while (last < 22 && ((cnk + (1ull << last) - 1) >> last) >= 2 * fl) last++;
+            while (wlevel < last && ((cnk + (1ull << wlevel) - 1) >> wlevel) > (1ull << 26)) wlevel++;
+            for (;;) {
+                cpb = std::min<uint64_t>(mine, std::max<uint64_t>(1, (1ull << 24) >> wlevel));
+                if ((cpb << wlevel) >= target || wlevel >= last) break;
+                wlevel++;
+            }
+            if (((cnk + (1ull << wlevel) - 1) >> wlevel) > (1ull << 26))
+                return fail(NICE_ERR_INVALID, "device MSD: chunk_size too large for the floor");
+            per = (cpb << wlevel) + 64;
+            // leaves of the BFS levels (clipped / depth-limited nodes), in pieces
+            wleaf_cap = per * (1 + (fl >> 28)) + 64;
+        }
         const uint64_t nbatches = nbatches_of(mine, cpb);
         for (size_t i = 0; i < ctx->devs.size(); i++) {
             Device &d = ctx->devs[i];
             HIPCHK(hipSetDevice(d.id));
             const uint64_t fgrid = std::min<uint64_t>(cpb, (uint64_t)d.num_cus * 4);
-            int r = fcap ? ensure_msd(d.slot[t], 0, (uint32_t)leaf_cap, fgrid * 2 * fcap)
-                         : ensure_msd(d.slot[t], (uint32_t)per, (uint32_t)leaf_cap, 0);
+            int r = fcap   ? ensure_msd(d.slot[t], 0, (uint32_t)leaf_cap, fgrid * 2 * fcap)
+                    : wave ? ensure_msd(d.slot[t], (uint32_t)per, (uint32_t)wleaf_cap, 0,
+                                        nice::msd_wave_scratch_bytes(wgrid))
+                           : ensure_msd(d.slot[t], (uint32_t)per, (uint32_t)leaf_cap, 0);
             if (r) return r;
             if (i < nbatches) {
                 job.used[i] = 1;
@@ -1152,11 +1194,28 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
 #ifdef NICE_PROBES
             mp.probe = getenv("NICE_MSD_PROBE") ? (uint32_t)atoi(getenv("NICE_MSD_PROBE")) : 0u;
 #endif
+            nice::NiceonlyLaunch p{};
+            if (wave) {
+                p.residues = mp.residues;
+                p.R = R;
+                p.M = (uint32_t)M;
+                p.base = base;
+                p.in_range = in_range;
+                p.out = nice::NumOut{d.slot[t].nice.n, nullptr, d.slot[t].d_nice_count, d.slot[t].nice.cap};
+                p.fin = last ? nice::NiceFinish{d.slot[t].d_msd_mapped, d.slot[t].d_nice_mapped, mb.counters,
+                                                d.slot[t].d_nice_done}
+                             : nice::NiceFinish{nullptr, nullptr, mb.counters, d.slot[t].d_nice_done};
+                hipError_t err = nice::launch_msd_wave(mp, p, wlevel, mb.wscratch, wgrid, d.num_cus,
+                                                       d.slot[t].nstream);
+                if (err != hipSuccess)
+                    return fail(NICE_ERR_HIP, std::string("msd wave launch: ") + hipGetErrorString(err));
+                st.launches++;
+                continue;
+            }
             const uint32_t fgrid = (uint32_t)std::min<uint64_t>(mp.nchunks, (uint64_t)d.num_cus * 4);
             hipError_t err = fcap ? nice::launch_msd_device(mp, d.num_cus, d.slot[t].nstream, mb.scratch, fcap, fgrid)
                                   : nice::launch_msd_device(mp, d.num_cus, d.slot[t].nstream);
             if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("msd launch: ") + hipGetErrorString(err));
-            nice::NiceonlyLaunch p{};
             p.leaves = mb.leaves;
             p.n_leaves_dev = mb.counters + 24;
             p.n_leaves = mb.leaf_cap;  // clamp for the device count

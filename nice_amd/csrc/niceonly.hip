@@ -42,6 +42,19 @@ __device__ __forceinline__ u32 lane_rank(u64 mask) {
     return __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u));
 }
 
+// LDS (and, with the workgroup-scope fence, global) accesses of one wave
+// ordered across its lanes: a wave runs in lockstep, so no barrier is needed.
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void wave_sync_global() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 __device__ __forceinline__ void emit_nice(const NiceonlyLaunch &p, u64 n_lo, u64 n_hi) {
     const u32 pos = atomicAdd(p.out.count, 1u);
     if (pos < p.out.cap) {
@@ -62,18 +75,123 @@ constexpr u32 kCubeQ = 128;
 template <int B>
 __device__ __forceinline__ void cube_pass(const NiceonlyLaunch &p, const ulonglong2 *q, u32 head, u32 cnt,
                                           u32 lane) {
-    // the queue was written by other lanes of this wave: order the LDS
-    // accesses (one wave, so no workgroup barrier)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_sync_lds();  // the queue was written by other lanes of this wave
     if (lane < cnt) {
         const ulonglong2 e = q[(head + lane) & (kCubeQ - 1)];
         if (is_nice_fast<B>(e.x, e.y)) emit_nice(p, e.x, e.y);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_sync_lds();
+}
+
+// Per-wave candidate state: the exact gi / R of the stride walk and the
+// square-survivor ring (head / tail wave-uniform).
+struct CandWave {
+    u64 r_magic;
+    u32 r_shift;
+    ulonglong2 *cq;
+    u32 q_head, q_tail;
+};
+__device__ __forceinline__ CandWave cand_wave(const NiceonlyLaunch &p, ulonglong2 *cq) {
+    // gi / R by one 32x32->64 multiply and a shift: gi = g0 + j < R + 2^28 <
+    // 2^29 and m = floor(2^s / R) + 1 with s = 30 + ceil(log2 R) keep the error
+    // below 2^-(L+1) <= 1/(2R), so the quotient is exact (m < 2^31 + 1).
+    const u32 r_log = 32 - __clz(p.R - 1);
+    return CandWave{(1ull << (30 + r_log)) / p.R + 1, 30 + r_log, cq, 0, 0};
+}
+
+// The stride candidates of LPW leaves (lane l < LPW holds leaf l, the others
+// count 0), 64 per round: lane k finds its leaf by a uniform binary search over
+// the wave's exclusive prefix (cross-lane reads), rebuilds n = b0 + ((g0 + j) /
+// R) * M + residues[(g0 + j) % R] and tests it (client_process.rs:222-253).
+template <class G, u32 LPW>
+__device__ __forceinline__ void check_leaf_group(const NiceonlyLaunch &p, const G &g, const Leaf &lf, u32 lane,
+                                                 CandWave &cw) {
+    u32 incl = lf.count;
+#pragma unroll
+    for (int o = 1; o < (int)LPW; o <<= 1) {
+        u32 v = __shfl_up(incl, o);
+        if (lane >= (u32)o) incl += v;
+    }
+    const u32 excl = incl - lf.count;
+    const u32 total = __shfl(incl, LPW - 1);
+    for (u32 r0 = 0; r0 < total; r0 += 64) {
+        const u32 k = r0 + lane;
+        // largest l < LPW with excl_l <= k (uniform search, all lanes active)
+        u32 lo = 0;
+#pragma unroll
+        for (u32 step = LPW / 2; step >= 1; step >>= 1) {
+            const u32 e = __shfl(excl, lo + step);
+            if (lo + step < LPW && e <= k) lo += step;
+        }
+        const u32 j = k - __shfl(excl, lo);
+        const u32 g0 = __shfl(lf.g0, lo);
+        const u64 b0lo = __shfl(lf.b0_lo, lo), b0hi = __shfl(lf.b0_hi, lo);
+        u64 n_lo = 0, n_hi = 0;
+        if (k < total) {
+            const u32 gi = g0 + j;
+            const u32 cyc = (u32)(((u64)gi * cw.r_magic) >> cw.r_shift);
+            const u32 idx = gi - cyc * p.R;
+            n_lo = b0lo;
+            n_hi = b0hi;
+            add_u128(n_lo, n_hi, (u64)cyc * p.M + p.residues[idx]);
+        }
+        if constexpr (IsConst<G>::value) {
+            if (p.in_range) {  // wave-uniform
+                // n^2 first; the few survivors queue for a full-wave cube pass
+                const bool sq = k < total && square_ok<IsConst<G>::base>(n_lo, n_hi);
+                const u64 bal = __ballot(sq);
+                if (bal) {
+                    if (sq) cw.cq[(cw.q_tail + lane_rank(bal)) & (kCubeQ - 1)] = make_ulonglong2(n_lo, n_hi);
+                    cw.q_tail += (u32)__popcll(bal);
+                    if (cw.q_tail - cw.q_head >= 64) {
+                        cube_pass<IsConst<G>::base>(p, cw.cq, cw.q_head, 64, lane);
+                        cw.q_head += 64;
+                    }
+                }
+                continue;
+            }
+        }
+        if (k < total && is_nice_dev(n_lo, n_hi, g)) emit_nice(p, n_lo, n_hi);
+    }
+}
+
+template <class G>
+__device__ __forceinline__ void cand_flush(const NiceonlyLaunch &p, CandWave &cw, u32 lane) {
+    if constexpr (IsConst<G>::value) {
+        if (cw.q_tail != cw.q_head) cube_pass<IsConst<G>::base>(p, cw.cq, cw.q_head, cw.q_tail - cw.q_head, lane);
+        cw.q_head = cw.q_tail;
+    }
+}
+
+// End of a niceonly launch (every thread of the workgroup calls it): the last
+// workgroup to retire copies the field's results to mapped host memory (the
+// count is agent-atomic, so: own atomics drained, barrier, one agent add per
+// workgroup -- no L2 write-back fence, see fd2's field_finish).  Field end
+// (count_mapped set): the MSD counters and the nice count out, then re-zeroed
+// for the slot's next field.  Batch end: only the per-batch leaf-record count
+// is re-zeroed, for the next batch.
+__device__ __forceinline__ void nice_launch_finish(const NiceFinish &fin, u32 *count) {
+    __shared__ u32 last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) last = last_block_arrive(fin.done);
+    __syncthreads();
+    if (!last) return;
+    u32 *ctr = fin.msd_counters;
+    const u32 w = threadIdx.x;
+    if (fin.count_mapped) {
+        if (ctr && w < 32) {
+            fin.msd_mapped[w] = __hip_atomic_load(&ctr[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (w >= 24) __hip_atomic_store(&ctr[w], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (w == 0) {
+            *fin.count_mapped = __hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else if (ctr && w == 24) {
+        __hip_atomic_store(&ctr[24], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    done_reset(fin.done);
 }
 
 template <class G>
@@ -83,17 +201,8 @@ niceonly_kernel(NiceonlyLaunch p, G g) {
     const u32 gwave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const u32 nwaves = (gridDim.x * blockDim.x) >> 6;
     const u32 n_leaves = p.n_leaves_dev ? min(*p.n_leaves_dev, p.n_leaves) : p.n_leaves;
-    // gi / R by one 32x32->64 multiply and a shift: gi = g0 + j < R + 2^28 <
-    // 2^29 and m = floor(2^s / R) + 1 with s = 30 + ceil(log2 R) keep the error
-    // below 2^-(L+1) <= 1/(2R), so the quotient is exact (m < 2^31 + 1).
-    const u32 r_log = 32 - __clz(p.R - 1);
-    const u64 r_magic = (1ull << (30 + r_log)) / p.R + 1;
-    const u32 r_shift = 30 + r_log;
-    // In-range fast bases: per-wave ring of the candidates whose square is
-    // repeat-free (see cube_pass); head / tail are wave-uniform.
     __shared__ ulonglong2 cq[4][IsConst<G>::value ? kCubeQ : 1];
-    const u32 wv = threadIdx.x >> 6;
-    u32 q_head = 0, q_tail = 0;
+    CandWave cw = cand_wave(p, cq[threadIdx.x >> 6]);
     // LPW leaves per wave (lanes >= LPW carry count 0): at the CPU path's
     // floor a leaf holds ~40 candidates, so 8 leaves keep a wave ~5 rounds
     // deep and spread a 35k-leaf field over ~4400 waves instead of ~550.
@@ -102,91 +211,10 @@ niceonly_kernel(NiceonlyLaunch p, G g) {
         const u32 li = base + lane;
         Leaf lf{0, 0, 0, 0};
         if (lane < LPW && li < n_leaves) lf = p.leaves[li];
-        // inclusive scan of counts across the wave
-        u32 incl = lf.count;
-#pragma unroll
-        for (int o = 1; o < (int)LPW; o <<= 1) {
-            u32 v = __shfl_up(incl, o);
-            if (lane >= (u32)o) incl += v;
-        }
-        const u32 excl = incl - lf.count;
-        const u32 total = __shfl(incl, LPW - 1);
-        for (u32 r0 = 0; r0 < total; r0 += 64) {
-            const u32 k = r0 + lane;
-            // largest l < LPW with excl_l <= k (uniform search, all lanes active)
-            u32 lo = 0;
-#pragma unroll
-            for (u32 step = LPW / 2; step >= 1; step >>= 1) {
-                const u32 e = __shfl(excl, lo + step);
-                if (lo + step < LPW && e <= k) lo += step;
-            }
-            const u32 j = k - __shfl(excl, lo);
-            const u32 g0 = __shfl(lf.g0, lo);
-            const u64 b0lo = __shfl(lf.b0_lo, lo), b0hi = __shfl(lf.b0_hi, lo);
-            u64 n_lo = 0, n_hi = 0;
-            if (k < total) {
-                const u32 gi = g0 + j;
-                const u32 cyc = (u32)(((u64)gi * r_magic) >> r_shift);
-                const u32 idx = gi - cyc * p.R;
-                n_lo = b0lo;
-                n_hi = b0hi;
-                add_u128(n_lo, n_hi, (u64)cyc * p.M + p.residues[idx]);
-            }
-            if constexpr (IsConst<G>::value) {
-                if (p.in_range) {  // wave-uniform
-                    // n^2 first; the few survivors queue for a full-wave cube pass
-                    const bool sq = k < total && square_ok<IsConst<G>::base>(n_lo, n_hi);
-                    const u64 bal = __ballot(sq);
-                    if (bal) {
-                        if (sq) {
-                            const u32 slot = (q_tail + lane_rank(bal)) & (kCubeQ - 1);
-                            cq[wv][slot] = make_ulonglong2(n_lo, n_hi);
-                        }
-                        q_tail += (u32)__popcll(bal);
-                        if (q_tail - q_head >= 64) {
-                            cube_pass<IsConst<G>::base>(p, cq[wv], q_head, 64, lane);
-                            q_head += 64;
-                        }
-                    }
-                    continue;
-                }
-            }
-            if (k < total && is_nice_dev(n_lo, n_hi, g)) emit_nice(p, n_lo, n_hi);
-        }
+        check_leaf_group<G, LPW>(p, g, lf, lane, cw);
     }
-    if constexpr (IsConst<G>::value) {
-        if (q_tail != q_head) cube_pass<IsConst<G>::base>(p, cq[wv], q_head, q_tail - q_head, lane);
-    }
-    if (p.fin.done) {
-        // last workgroup: the field's results to mapped host memory (the
-        // count is agent-atomic, so: own atomics drained, barrier, one agent
-        // add per workgroup -- no L2 write-back fence, see fd2's field_finish)
-        __shared__ u32 last;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) last = last_block_arrive(p.fin.done);
-        __syncthreads();
-        if (last) {
-            // Field end (count_mapped set): results out, then the field's
-            // counters re-zeroed for the slot's next field.  Batch end: only
-            // the per-batch leaf-record count, for the next batch.
-            u32 *ctr = p.fin.msd_counters;
-            const u32 w = threadIdx.x;
-            if (p.fin.count_mapped) {
-                if (ctr && w < 32) {
-                    p.fin.msd_mapped[w] = __hip_atomic_load(&ctr[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (w >= 24) __hip_atomic_store(&ctr[w], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                if (w == 0) {
-                    *p.fin.count_mapped = __hip_atomic_load(p.out.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(p.out.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            } else if (ctr && w == 24) {
-                __hip_atomic_store(&ctr[24], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            done_reset(p.fin.done);
-        }
-    }
+    cand_flush<G>(p, cw, lane);
+    if (p.fin.done) nice_launch_finish(p.fin, p.out.count);
 }
 
 __global__ void is_nice_kernel(const u64 *n_pairs, u32 count, GenericBase g, u32 *out) {
@@ -511,7 +539,9 @@ msd_level_kernel(MsdLaunch p, u32 level, G g) {
     if (threadIdx.x < 3) stat[threadIdx.x] = 0;
     const MsdNode *qin = p.q[level & 1];
     MsdNode *qout = p.q[(level + 1) & 1];
-    const u32 n_in = p.counters[level];
+    // (an overflowed level leaves its count above the queue: flagged, and
+    // never read past)
+    const u32 n_in = min(p.counters[level], p.q_cap);
     // Workgroup-uniform loop: leaves and children are appended with one atomic
     // per workgroup, statistics summed in LDS and added once at the end.
     const u32 stride = gridDim.x * blockDim.x;
@@ -613,6 +643,133 @@ msd_fused_kernel(MsdLaunch p, ChunkNode *scratch, u32 cap, G g) {
     flush_stats(p, n_st, c_st, s_st, stat);
 }
 
+// MSD recursion and candidate test fused, one wave per subtree stream, for
+// chunks too large for msd_fused_kernel (the massive field's 1e8 chunks).
+// The level BFS above it runs only the first few levels (until a batch has
+// tens of thousands of nodes of <= 2^26 numbers); each wave then takes those
+// roots grid-strided and recurses with a wave-private work stack in global
+// memory: pop up to 64 nodes (one per lane), classify (the reference's node
+// rule), push the split nodes' halves.  The stack is topped up with fresh
+// roots whenever it holds fewer than 64 nodes, so lanes stay busy across
+// small subtrees.  Leaves never leave the wave: their stride descriptors queue
+// in LDS and are tested 64 at a time by the candidate code above (square
+// first, cube on a full wave of survivors).  No leaf list, no level launches
+// below the roots, and no same-address atomic per level iteration: the level
+// BFS spent most of its 85 ms on the massive field in launches and in the
+// L2-serialised queue and statistics atomics of ~10^4 small launches.
+struct StackNode {
+    u64 off;    // from the field start
+    u32 size;   // <= 2^26 (the host picks the root level for it)
+    u32 depth;  // recursion level (the reference's depth, <= 22)
+};
+// Work stack per wave: a pop takes <= 64 nodes off the top and pushes <= 128
+// one level deeper, so at most ~64 nodes per level stay behind (23 levels) plus
+// one refill of 64 roots; overflow sets the MSD overflow flag (an error).
+constexpr u32 kStackCap = 2048;
+// Leaf-descriptor queue per wave: tested 64 at a time, in groups of 16.
+constexpr u32 kLeafQ = 128, kLeafGroup = 16;
+
+template <class G, u32 MC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+msd_wave_kernel(MsdLaunch p, NiceonlyLaunch c, u32 level0, StackNode *scratch, G g) {
+    __shared__ ulonglong2 cq[4][IsConst<G>::value ? kCubeQ : 1];
+    __shared__ Leaf lq[4][kLeafQ];
+    __shared__ unsigned long long stat[3];
+    if (threadIdx.x < 3) stat[threadIdx.x] = 0;
+    const u32 lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const u64 gwave = (u64)blockIdx.x * 4 + wv, nwaves = (u64)gridDim.x * 4;
+    StackNode *st = scratch + gwave * kStackCap;
+    Leaf *q = lq[wv];
+    CandWave cw = cand_wave(c, cq[wv]);
+    u64 n_st = 0, c_st = 0, s_st = 0;
+
+    // Leaves the BFS levels above produced (clipped or depth-limited nodes):
+    // already stride descriptors in the batch's leaf list.
+    const u32 n_list = min(p.counters[24], p.leaf_cap);
+    for (u64 b = gwave * kLeafGroup; b < n_list; b += nwaves * kLeafGroup) {
+        Leaf lf{0, 0, 0, 0};
+        if (lane < kLeafGroup && b + lane < n_list) lf = p.leaves[b + lane];
+        check_leaf_group<G, kLeafGroup>(c, g, lf, lane, cw);
+    }
+
+    const MsdNode *roots = p.q[level0 & 1];
+    const u64 n_roots = min(p.counters[level0], p.q_cap);
+    u64 next = gwave;    // next root of this wave (grid-strided)
+    u32 sp = 0;          // stack depth (wave-uniform)
+    u32 lq_head = 0, lq_tail = 0;
+    for (;;) {
+        if (sp < 64 && next < n_roots) {  // top up with roots
+            const u64 ri = next + (u64)lane * nwaves;
+            const bool ok = lane < 64 - sp && ri < n_roots;
+            if (ok) {
+                const MsdNode r = roots[ri];
+                st[sp + lane] = StackNode{r.off, (u32)r.size, level0};
+            }
+            const u32 got = (u32)__popcll(__ballot(ok));
+            next += (u64)got * nwaves;
+            sp += got;
+            wave_sync_global();
+        }
+        if (sp == 0) break;
+        const u32 cnt = sp < 64 ? sp : 64;
+        sp -= cnt;
+        StackNode nd{0, 0, 0};
+        if (lane < cnt) nd = st[sp + lane];
+        wave_sync_global();  // popped before the pushes below reuse the slots
+        u64 lo = p.start_lo, hi = p.start_hi;
+        add_u128(lo, hi, nd.off);
+        const u32 act = lane < cnt ? classify_node(p, nd.depth, lo, hi, nd.size, g) : 0u;
+        // a leaf: its stride descriptor to the queue (statistics as the
+        // reference counts them: every MSD-surviving range)
+        LeafDesc ld{0, 0, 0, 0};
+        if (act == 1) {
+            ld = leaf_desc<MC>(lo, hi, nd.size, p);
+            n_st++;
+            c_st += ld.count;
+            s_st += nd.size;
+        }
+        const bool put = act == 1 && ld.count != 0;
+        const u64 bl = __ballot(put);
+        if (put) q[(lq_tail + lane_rank(bl)) & (kLeafQ - 1)] = Leaf{ld.b0_lo, ld.b0_hi, ld.g0, (u32)ld.count};
+        lq_tail += (u32)__popcll(bl);
+        // a split: both halves on the stack, one level deeper
+        const u64 bs = __ballot(act == 2);
+        const u32 nsplit = (u32)__popcll(bs);
+        if (sp + 2 * nsplit > kStackCap) {
+            if (lane == 0) atomicOr(&p.counters[25], 1u);  // reported as an error by the host
+        } else {
+            if (act == 2) {
+                const u32 r = sp + 2 * lane_rank(bs), half = nd.size / 2;
+                st[r] = StackNode{nd.off, half, nd.depth + 1};
+                st[r + 1] = StackNode{nd.off + half, nd.size - half, nd.depth + 1};
+            }
+            sp += 2 * nsplit;
+        }
+        wave_sync_global();
+        // test queued leaves 64 at a time
+        if (lq_tail - lq_head >= 64) {
+            wave_sync_lds();
+            for (u32 gq = 0; gq < 64; gq += kLeafGroup) {
+                Leaf lf{0, 0, 0, 0};
+                if (lane < kLeafGroup) lf = q[(lq_head + gq + lane) & (kLeafQ - 1)];
+                check_leaf_group<G, kLeafGroup>(c, g, lf, lane, cw);
+            }
+            lq_head += 64;
+        }
+    }
+    wave_sync_lds();
+    while (lq_head != lq_tail) {
+        const u32 n = lq_tail - lq_head < kLeafGroup ? lq_tail - lq_head : kLeafGroup;
+        Leaf lf{0, 0, 0, 0};
+        if (lane < n) lf = q[(lq_head + lane) & (kLeafQ - 1)];
+        check_leaf_group<G, kLeafGroup>(c, g, lf, lane, cw);
+        lq_head += n;
+    }
+    cand_flush<G>(c, cw, lane);
+    flush_stats(p, n_st, c_st, s_st, stat);
+    if (c.fin.done) nice_launch_finish(c.fin, c.out.count);
+}
+
 // ---------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------
@@ -686,6 +843,39 @@ static hipError_t launch_fused(const MsdLaunch &p, const G &g, ChunkNode *scratc
     hipLaunchKernelGGL((msd_fused_kernel<G, MC>), dim3(grid), dim3(256), 0, s, p, scratch, cap, g);
     return hipGetLastError();
 }
+
+template <class G, u32 MC = 0>
+static hipError_t launch_wave(const MsdLaunch &p, const NiceonlyLaunch &c, u32 level0, StackNode *scratch,
+                              u32 grid, const G &g, int num_cus, hipStream_t s) {
+    hipLaunchKernelGGL(msd_init_kernel, dim3(256), dim3(256), 0, s, p);
+    for (u32 level = 0; level < level0; level++) {
+        const u64 nodes = p.nchunks << level;
+        u64 lgrid = (nodes + 255) / 256;
+        const u64 cap = (u64)num_cus * 2;
+        if (lgrid > cap) lgrid = cap;
+        hipLaunchKernelGGL((msd_level_kernel<G, MC>), dim3((u32)lgrid), dim3(256), 0, s, p, level, g);
+    }
+    hipLaunchKernelGGL((msd_wave_kernel<G, MC>), dim3(grid), dim3(256), 0, s, p, c, level0, scratch, g);
+    return hipGetLastError();
+}
+
+hipError_t launch_msd_wave(const MsdLaunch &p, const NiceonlyLaunch &c, uint32_t level0, void *scratch,
+                           uint32_t grid, int num_cus, hipStream_t s) {
+    if (level0 > 22 || (p.nchunks << level0) >> level0 != p.nchunks) return hipErrorInvalidValue;
+    StackNode *st = (StackNode *)scratch;
+    switch (p.base) {
+#define X(b)                                                                                        \
+    case b:                                                                                          \
+        if (const_modulus<b>() && p.in_range && p.M == const_modulus<b>())                         \
+            return launch_wave<ConstBase<b>, const_modulus<b>()>(p, c, level0, st, grid, ConstBase<b>{}, num_cus, s); \
+        return launch_wave(p, c, level0, st, grid, ConstBase<b>{}, num_cus, s);
+        NICE_NICEONLY_BASES(X)
+#undef X
+    default: return launch_wave(p, c, level0, st, grid, make_generic(p.base), num_cus, s);
+    }
+}
+
+size_t msd_wave_scratch_bytes(uint32_t grid) { return (size_t)grid * 4 * kStackCap * sizeof(StackNode); }
 
 u32 msd_fused_cap(u64 chunk, u64 floor_size) {
     if (chunk > 0xffffffffull || floor_size == 0) return 0;

@@ -63,18 +63,42 @@ __host__ __device__ __forceinline__ bool moverlap(const u32 (&a)[MW], const u32 
     return o != 0;
 }
 
+// B^e fits 32 bits (B^e <= 2^32).
+constexpr bool pow_le32(unsigned long long b, int e) {
+    unsigned long long v = 1;
+    for (int i = 0; i < e; i++) {
+        v *= b;
+        if (v > (1ull << 32)) return false;
+    }
+    return true;
+}
+
 // n (in range, < B^NX) as NX radix-B limbs.
 template <int BASE>
 __host__ __device__ __forceinline__ void to_limbs(u64 lo, u64 hi, u32 (&X)[Radix<BASE>::NX]) {
     constexpr u32 B = Radix<BASE>::B;
     if constexpr (Radix<BASE>::FITS64) {  // n < B^NX < 2^64 (b40, b50)
+        // two limbs per u64 division by B^2 (< 2^32), the pair split in 32
+        // bits; once the rest fits 32 bits (B^(NX-j) <= 2^32) all in 32 bits
         (void)hi;
+        constexpr u64 B2 = (u64)B * B;
         u64 v = lo;
 #pragma unroll
-        for (int j = 0; j < Radix<BASE>::NX; j++) {
-            const u64 q = v / B;
-            X[j] = (u32)(v - q * B);
-            v = q;
+        for (int j = 0; j < Radix<BASE>::NX; j += 2) {
+            if (j + 1 == Radix<BASE>::NX) {  // the top limb: v < B
+                X[j] = (u32)v;
+            } else if (pow_le32(B, Radix<BASE>::NX - j)) {
+                const u32 w = (u32)v, q = w / (u32)B2, r = w - q * (u32)B2;
+                X[j] = r % B;
+                X[j + 1] = r / B;
+                v = q;
+            } else {
+                const u64 q = v / B2;
+                const u32 r = (u32)(v - q * B2);
+                X[j] = r % B;
+                X[j + 1] = r / B;
+                v = q;
+            }
         }
     } else {
         u32 w[4] = {(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
