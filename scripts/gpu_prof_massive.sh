@@ -13,7 +13,7 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SAL
            "VALUBusy" "GRBM_GUI_ACTIVE GRBM_COUNT SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $O/pmc_massive_$i -o p -- python3 $R/scripts/massive_1gpu.py 10 > $O/pmc_massive_$i.log 2>&1
-  for k in niceonly_kernel msd_level_kernel msd_fused_kernel; do
+  for k in niceonly_kernel msd_level_kernel msd_fused_kernel msd_wave_kernel; do
     python3 $R/scripts/pmc_sum_all.py $k $O/pmc_massive_$i/p_counter_collection.csv >> $O/pmc_massive_summary.txt
   done
   rm -f $O/pmc_massive_$i/p_counter_collection.csv
