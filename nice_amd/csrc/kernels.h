@@ -160,6 +160,7 @@ hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s, Chu
 hipError_t launch_msd_wave(const MsdLaunch &p, const NiceonlyLaunch &c, uint32_t level0, void *scratch,
                            uint32_t grid, int num_cus, hipStream_t s);
 size_t msd_wave_scratch_bytes(uint32_t grid);
+uint32_t msd_wave_waves_per_group();
 
 // Diagnostics used by the parity tests: per-n unique counts / nice flags
 // computed by the same device functions the production kernels use.

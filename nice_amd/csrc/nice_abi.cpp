@@ -1125,12 +1125,13 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
         if (wave) {
             int cus = 256;
             for (auto &d : ctx->devs) cus = std::max(cus, d.num_cus);
-            wgrid = (uint32_t)cus * 4;
+            wgrid = (uint32_t)cus * 16 / nice::msd_wave_waves_per_group();  // 4 waves per SIMD
             // roots per wave: 2048 (the whole massive field 0.097 s at 32, 0.080 s
             // at 2048; a 1/8 dealt share 0.0135 / 0.0101 s, scripts/roots_sweep.py)
-            uint64_t target = (uint64_t)wgrid * 4 * 2048;
+            const uint64_t waves = (uint64_t)wgrid * nice::msd_wave_waves_per_group();
+            uint64_t target = waves * 2048;
 #ifdef NICE_PROBES
-            if (getenv("NICE_MSD_ROOTS")) target = (uint64_t)wgrid * 4 * strtoull(getenv("NICE_MSD_ROOTS"), nullptr, 10);
+            if (getenv("NICE_MSD_ROOTS")) target = waves * strtoull(getenv("NICE_MSD_ROOTS"), nullptr, 10);
 #endif
             uint32_t last = 0;  // first level without splits
             while (last < 22 && ((cnk + (1ull << last) - 1) >> last) >= 2 * fl) last++;

@@ -67,6 +67,26 @@ __device__ __forceinline__ void emit_nice(const NiceonlyLaunch &p, u64 n_lo, u64
 // at most 64 to fewer than 64 queued).
 constexpr u32 kCubeQ = 128;
 
+// LDS pair-mask table of the in-range test (two-word fast bases): entries
+// per base, 1 (unused) otherwise.
+template <class G>
+struct PairTab {
+    static constexpr bool on = IsConst<G>::value && IsConst<G>::base > 32 && IsConst<G>::base <= 64;
+    static constexpr u32 N = on ? (u32)IsConst<G>::base * IsConst<G>::base : 1u;
+};
+// Every thread of the workgroup calls it (ends with a barrier).
+template <class G>
+__device__ __forceinline__ void pair_tab_fill(uint2 *tab) {
+    if constexpr (PairTab<G>::on) {
+        constexpr u32 b = IsConst<G>::base;
+        for (u32 e = threadIdx.x; e < PairTab<G>::N; e += blockDim.x) {
+            const u64 bits = (1ull << (e % b)) | (1ull << (e / b));
+            tab[e] = make_uint2((u32)bits, (u32)(bits >> 32));
+        }
+    }
+    __syncthreads();
+}
+
 // The full niceness test on `cnt` <= 64 queued candidates, one per lane.  At
 // the MSD floor about one stride candidate in ~20 has a repeat-free square
 // (the MSD filter already vetted the leading digits), yet nearly every round of
@@ -74,11 +94,14 @@ constexpr u32 kCubeQ = 128;
 // almost every wave and round.  Queued, it runs once per 64 survivors.
 template <int B>
 __device__ __forceinline__ void cube_pass(const NiceonlyLaunch &p, const ulonglong2 *q, u32 head, u32 cnt,
-                                          u32 lane) {
+                                          u32 lane, const uint2 *tab) {
     wave_sync_lds();  // the queue was written by other lanes of this wave
     if (lane < cnt) {
         const ulonglong2 e = q[(head + lane) & (kCubeQ - 1)];
-        if (is_nice_fast<B>(e.x, e.y)) emit_nice(p, e.x, e.y);
+        bool nice;
+        if constexpr (B > 32 && B <= 64) nice = is_nice_tab<B>(e.x, e.y, tab);
+        else nice = is_nice_fast<B>(e.x, e.y);
+        if (nice) emit_nice(p, e.x, e.y);
     }
     wave_sync_lds();
 }
@@ -89,14 +112,15 @@ struct CandWave {
     u64 r_magic;
     u32 r_shift;
     ulonglong2 *cq;
+    const uint2 *tab;  // LDS pair-mask table (PairTab), or unused
     u32 q_head, q_tail;
 };
-__device__ __forceinline__ CandWave cand_wave(const NiceonlyLaunch &p, ulonglong2 *cq) {
+__device__ __forceinline__ CandWave cand_wave(const NiceonlyLaunch &p, ulonglong2 *cq, const uint2 *tab) {
     // gi / R by one 32x32->64 multiply and a shift: gi = g0 + j < R + 2^28 <
     // 2^29 and m = floor(2^s / R) + 1 with s = 30 + ceil(log2 R) keep the error
     // below 2^-(L+1) <= 1/(2R), so the quotient is exact (m < 2^31 + 1).
     const u32 r_log = 32 - __clz(p.R - 1);
-    return CandWave{(1ull << (30 + r_log)) / p.R + 1, 30 + r_log, cq, 0, 0};
+    return CandWave{(1ull << (30 + r_log)) / p.R + 1, 30 + r_log, cq, tab, 0, 0};
 }
 
 // The stride candidates of LPW leaves (lane l < LPW holds leaf l, the others
@@ -138,13 +162,17 @@ __device__ __forceinline__ void check_leaf_group(const NiceonlyLaunch &p, const 
         if constexpr (IsConst<G>::value) {
             if (p.in_range) {  // wave-uniform
                 // n^2 first; the few survivors queue for a full-wave cube pass
-                const bool sq = k < total && square_ok<IsConst<G>::base>(n_lo, n_hi);
+                bool sq = false;
+                if (k < total) {
+                    if constexpr (PairTab<G>::on) sq = square_ok_tab<IsConst<G>::base>(n_lo, n_hi, cw.tab);
+                    else sq = square_ok<IsConst<G>::base>(n_lo, n_hi);
+                }
                 const u64 bal = __ballot(sq);
                 if (bal) {
                     if (sq) cw.cq[(cw.q_tail + lane_rank(bal)) & (kCubeQ - 1)] = make_ulonglong2(n_lo, n_hi);
                     cw.q_tail += (u32)__popcll(bal);
                     if (cw.q_tail - cw.q_head >= 64) {
-                        cube_pass<IsConst<G>::base>(p, cw.cq, cw.q_head, 64, lane);
+                        cube_pass<IsConst<G>::base>(p, cw.cq, cw.q_head, 64, lane, cw.tab);
                         cw.q_head += 64;
                     }
                 }
@@ -158,7 +186,8 @@ __device__ __forceinline__ void check_leaf_group(const NiceonlyLaunch &p, const 
 template <class G>
 __device__ __forceinline__ void cand_flush(const NiceonlyLaunch &p, CandWave &cw, u32 lane) {
     if constexpr (IsConst<G>::value) {
-        if (cw.q_tail != cw.q_head) cube_pass<IsConst<G>::base>(p, cw.cq, cw.q_head, cw.q_tail - cw.q_head, lane);
+        if (cw.q_tail != cw.q_head)
+            cube_pass<IsConst<G>::base>(p, cw.cq, cw.q_head, cw.q_tail - cw.q_head, lane, cw.tab);
         cw.q_head = cw.q_tail;
     }
 }
@@ -202,7 +231,9 @@ niceonly_kernel(NiceonlyLaunch p, G g) {
     const u32 nwaves = (gridDim.x * blockDim.x) >> 6;
     const u32 n_leaves = p.n_leaves_dev ? min(*p.n_leaves_dev, p.n_leaves) : p.n_leaves;
     __shared__ ulonglong2 cq[4][IsConst<G>::value ? kCubeQ : 1];
-    CandWave cw = cand_wave(p, cq[threadIdx.x >> 6]);
+    __shared__ uint2 tab[PairTab<G>::N];
+    pair_tab_fill<G>(tab);
+    CandWave cw = cand_wave(p, cq[threadIdx.x >> 6], tab);
     // LPW leaves per wave (lanes >= LPW carry count 0): at the CPU path's
     // floor a leaf holds ~40 candidates, so 8 leaves keep a wave ~5 rounds
     // deep and spread a 35k-leaf field over ~4400 waves instead of ~550.
@@ -668,19 +699,30 @@ struct StackNode {
 constexpr u32 kStackCap = 2048;
 // Leaf-descriptor queue per wave: tested 64 at a time, in groups of 16.
 constexpr u32 kLeafQ = 128, kLeafGroup = 16;
+// 512-thread workgroups: the pair table (<= 23 KB) is shared by 8 waves, two
+// workgroups per CU at 4 waves per SIMD.
+constexpr u32 kWaveWG = 512;
+
+// 4 waves per SIMD (<= 128 VGPRs) where the base's limb arrays allow it
+// without spilling; the three-word b80 path needs ~220.
+template <class G>
+constexpr int wave_occupancy() { return IsConst<G>::value && IsConst<G>::base > 64 ? 2 : 4; }
 
 template <class G, u32 MC>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ void __launch_bounds__(kWaveWG) __attribute__((amdgpu_waves_per_eu(wave_occupancy<G>())))
 msd_wave_kernel(MsdLaunch p, NiceonlyLaunch c, u32 level0, StackNode *scratch, G g) {
-    __shared__ ulonglong2 cq[4][IsConst<G>::value ? kCubeQ : 1];
-    __shared__ Leaf lq[4][kLeafQ];
+    constexpr u32 W = kWaveWG / 64;
+    __shared__ ulonglong2 cq[W][IsConst<G>::value ? kCubeQ : 1];
+    __shared__ Leaf lq[W][kLeafQ];
+    __shared__ uint2 tab[PairTab<G>::N];
     __shared__ unsigned long long stat[3];
     if (threadIdx.x < 3) stat[threadIdx.x] = 0;
+    pair_tab_fill<G>(tab);
     const u32 lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const u64 gwave = (u64)blockIdx.x * 4 + wv, nwaves = (u64)gridDim.x * 4;
+    const u64 gwave = (u64)blockIdx.x * W + wv, nwaves = (u64)gridDim.x * W;
     StackNode *st = scratch + gwave * kStackCap;
     Leaf *q = lq[wv];
-    CandWave cw = cand_wave(c, cq[wv]);
+    CandWave cw = cand_wave(c, cq[wv], tab);
     u64 n_st = 0, c_st = 0, s_st = 0;
 
     // Leaves the BFS levels above produced (clipped or depth-limited nodes):
@@ -855,7 +897,7 @@ static hipError_t launch_wave(const MsdLaunch &p, const NiceonlyLaunch &c, u32 l
         if (lgrid > cap) lgrid = cap;
         hipLaunchKernelGGL((msd_level_kernel<G, MC>), dim3((u32)lgrid), dim3(256), 0, s, p, level, g);
     }
-    hipLaunchKernelGGL((msd_wave_kernel<G, MC>), dim3(grid), dim3(256), 0, s, p, c, level0, scratch, g);
+    hipLaunchKernelGGL((msd_wave_kernel<G, MC>), dim3(grid), dim3(kWaveWG), 0, s, p, c, level0, scratch, g);
     return hipGetLastError();
 }
 
@@ -875,7 +917,8 @@ hipError_t launch_msd_wave(const MsdLaunch &p, const NiceonlyLaunch &c, uint32_t
     }
 }
 
-size_t msd_wave_scratch_bytes(uint32_t grid) { return (size_t)grid * 4 * kStackCap * sizeof(StackNode); }
+size_t msd_wave_scratch_bytes(uint32_t grid) { return (size_t)grid * (kWaveWG / 64) * kStackCap * sizeof(StackNode); }
+uint32_t msd_wave_waves_per_group() { return kWaveWG / 64; }
 
 u32 msd_fused_cap(u64 chunk, u64 floor_size) {
     if (chunk > 0xffffffffull || floor_size == 0) return 0;

@@ -189,6 +189,24 @@ __host__ __device__ __forceinline__ u32 limbs_popcount(const u32 (&A)[N], int D,
     return c;
 }
 
+// Two-word bases: each limb's two digit bits from a pair-mask table in LDS
+// (entry v marks v's digits v / b and v % b; one ds_read_b64 instead of ~7
+// VALU).  A top limb holding one digit keeps the VALU path.
+template <int BASE, int N>
+__device__ __forceinline__ u32 limbs_popcount_tab(const u32 (&A)[N], int D, u32 (&m)[2], const uint2 *tab) {
+#pragma unroll
+    for (int t = 0; t < N; t++) {
+        if (2 * t + 1 < D) {
+            const uint2 e = tab[A[t]];
+            m[0] |= e.x;
+            m[1] |= e.y;
+        } else {
+            or_limb<BASE>(A[t], false, m);
+        }
+    }
+    return popc32(m[0]) + popc32(m[1]);
+}
+
 // get_is_nice (client_process.rs:222-253) for in-range n.  Inside the valid
 // range n^2 and n^3 have exactly D2 + D3 = b digits, so "no digit repeats"
 // (the reference's early-exit scan, n^2 then n^3) is "the union of their
@@ -228,6 +246,30 @@ __host__ __device__ __forceinline__ bool is_nice_fast(u64 lo, u64 hi) {
     u32 X[Radix<BASE>::NX];
     to_limbs<BASE>(lo, hi, X);
     return is_nice_limbs<BASE>(X);
+}
+
+// The same two tests with the LDS pair table (two-word bases, see above).
+template <int BASE>
+__device__ __forceinline__ bool square_ok_tab(u64 lo, u64 hi, const uint2 *tab) {
+    using R = Radix<BASE>;
+    static_assert(R::MW == 2, "pair table: two-word bases");
+    u32 X[R::NX], S[R::NS];
+    to_limbs<BASE>(lo, hi, X);
+    square_limbs<BASE>(X, S);
+    u32 m[2] = {0, 0};
+    return limbs_popcount_tab<BASE>(S, R::D2, m, tab) == (u32)R::D2;
+}
+template <int BASE>
+__device__ __forceinline__ bool is_nice_tab(u64 lo, u64 hi, const uint2 *tab) {
+    using R = Radix<BASE>;
+    static_assert(R::MW == 2, "pair table: two-word bases");
+    u32 X[R::NX], S[R::NS], C[R::NC];
+    to_limbs<BASE>(lo, hi, X);
+    square_limbs<BASE>(X, S);
+    u32 m[2] = {0, 0};
+    if (limbs_popcount_tab<BASE>(S, R::D2, m, tab) != (u32)R::D2) return false;
+    cube_limbs<BASE>(S, X, C);
+    return limbs_popcount_tab<BASE>(C, R::D3, m, tab) == (u32)BASE;
 }
 
 // Unique-digit count of in-range n by the same limb path (test hook: checks
