@@ -131,7 +131,8 @@ struct MsdLaunch {
     uint32_t in_range;            // the batch lies inside the base's valid range
     uint32_t first_batch;         // init zeroes the field's sticky counters and *nice_count
     uint32_t *nice_count;
-    uint32_t probe;               // probe build only (NICE_MSD_PROBE): 1 no skip test, 2 no leaf stride math
+    uint32_t probe;               // probe build only (NICE_MSD_PROBE): 1 no skip test, 2 no leaf stride math,
+                                  // 4 wave kernel: no candidate test
 };
 // A leaf's candidate count is capped at kLeafPiece: longer runs are stored as
 // several leaves, so niceonly_kernel's per-wave sums of 8 leaves fit 32 bits.

@@ -474,9 +474,9 @@ __device__ __forceinline__ u32 block_reserve(u32 *ctr, u32 mine, u32 *slots) {
 
 // The recursion's rule for one node (msd_prefix_filter.rs:583-658):
 // 0 = dropped (has_duplicate_msd_prefix), 1 = leaf, 2 = split in two.
-template <class G>
+template <class G, bool TAB = false>
 __device__ __forceinline__ u32 classify_node(const MsdLaunch &p, u32 level, u64 lo, u64 hi, u64 size,
-                                             const G &g) {
+                                             const G &g, const uint2 *tab = nullptr) {
     bool leaf = level >= 22 || size <= p.floor_size;
     if (leaf) return 1;
     u64 l_lo = lo, l_hi = hi;
@@ -489,7 +489,7 @@ __device__ __forceinline__ u32 classify_node(const MsdLaunch &p, u32 level, u64 
     bool skip = false;
     if (size != 1 && !no_skip_test) {
         if constexpr (IsConst<G>::value) {
-            skip = p.in_range ? msd_skippable_fast<IsConst<G>::base>(lo, hi, l_lo, l_hi)
+            skip = p.in_range ? msd_skippable_fast<IsConst<G>::base, TAB>(lo, hi, l_lo, l_hi, tab)
                               : msd_skippable<G>(lo, hi, l_lo, l_hi, g);
         } else {
             skip = msd_skippable<G>(lo, hi, l_lo, l_hi, g);
@@ -703,6 +703,76 @@ constexpr u32 kLeafQ = 128, kLeafGroup = 16;
 // workgroups per CU at 4 waves per SIMD.
 constexpr u32 kWaveWG = 512;
 
+// Lane walk (two-word in-range bases whose n fit 64 bits: the wave kernel's
+// const-modulus instantiations).  Each lane takes one leaf from the wave's
+// queue and tests one of its candidates per round, stepping the residue index
+// (no division, no search) and taking the next queued leaf when its own runs
+// out.  The packed walk of check_leaf_group spends ~10 cross-lane reads per
+// round locating each lane's leaf (a binary search over the group's prefix,
+// then the leaf's fields).  Queue entries are 16 bytes; the queue is walked
+// once it holds kWalkAt leaves (>= 3 per lane, so lanes rarely idle at the
+// end).  Massive field: 0.0688 -> 0.0652 s.  (Loading the next round's
+// residue ahead of the current test gained nothing: not latency-bound.)
+struct LeafW {
+    u64 b0;
+    u32 g0, count;
+};
+constexpr u32 kWalkQ = 256, kWalkAt = 192;
+
+template <int B>
+__device__ __forceinline__ void walk_leaves(const NiceonlyLaunch &c, const LeafW *q, u32 head, u32 n, u32 lane,
+                                            CandWave &cw) {
+    wave_sync_lds();  // queue entries written by other lanes
+    u32 taken = 0;    // wave-uniform
+    bool have = false;
+    u64 cb = 0;  // the candidate's cycle base b0 + k M
+    u32 idx = 0, left = 0;
+    for (;;) {
+        const u64 need = __ballot(!have);
+        if (need && taken < n) {  // lanes without a leaf take the next ones
+            const u32 r = lane_rank(need);
+            if (!have && taken + r < n) {
+                const LeafW e = q[(head + taken + r) & (kWalkQ - 1)];
+                cb = e.b0;
+                idx = e.g0;
+                left = e.count;
+                if (idx >= c.R) {  // g0 == R: the first candidate is in the next cycle
+                    idx -= c.R;
+                    cb += c.M;
+                }
+                have = left != 0;
+            }
+            const u32 np = (u32)__popcll(need);
+            taken = n - taken > np ? taken + np : n;
+        }
+        if (!__ballot(have)) {
+            if (taken >= n) break;
+            continue;
+        }
+        u64 nv = 0;
+        bool sq = false;
+        if (have) {
+            nv = cb + c.residues[idx];
+            sq = square_ok_tab<B>(nv, 0, cw.tab);
+            if (++idx == c.R) {
+                idx = 0;
+                cb += c.M;
+            }
+            have = --left != 0;
+        }
+        const u64 bal = __ballot(sq);
+        if (bal) {
+            if (sq) cw.cq[(cw.q_tail + lane_rank(bal)) & (kCubeQ - 1)] = make_ulonglong2(nv, 0ull);
+            cw.q_tail += (u32)__popcll(bal);
+            if (cw.q_tail - cw.q_head >= 64) {
+                cube_pass<B>(c, cw.cq, cw.q_head, 64, lane, cw.tab);
+                cw.q_head += 64;
+            }
+        }
+    }
+    wave_sync_lds();
+}
+
 // 4 waves per SIMD (<= 128 VGPRs) where the base's limb arrays allow it
 // without spilling; the three-word b80 path needs ~220.
 template <class G>
@@ -712,8 +782,10 @@ template <class G, u32 MC>
 __global__ void __launch_bounds__(kWaveWG) __attribute__((amdgpu_waves_per_eu(wave_occupancy<G>())))
 msd_wave_kernel(MsdLaunch p, NiceonlyLaunch c, u32 level0, StackNode *scratch, G g) {
     constexpr u32 W = kWaveWG / 64;
+    constexpr bool WALK = PairTab<G>::on && MC != 0;  // lane walk (see walk_leaves)
     __shared__ ulonglong2 cq[W][IsConst<G>::value ? kCubeQ : 1];
-    __shared__ Leaf lq[W][kLeafQ];
+    __shared__ Leaf lq[W][WALK ? 1 : kLeafQ];
+    __shared__ LeafW lw[W][WALK ? kWalkQ : 1];
     __shared__ uint2 tab[PairTab<G>::N];
     __shared__ unsigned long long stat[3];
     if (threadIdx.x < 3) stat[threadIdx.x] = 0;
@@ -722,6 +794,7 @@ msd_wave_kernel(MsdLaunch p, NiceonlyLaunch c, u32 level0, StackNode *scratch, G
     const u64 gwave = (u64)blockIdx.x * W + wv, nwaves = (u64)gridDim.x * W;
     StackNode *st = scratch + gwave * kStackCap;
     Leaf *q = lq[wv];
+    LeafW *qw = lw[wv];
     CandWave cw = cand_wave(c, cq[wv], tab);
     u64 n_st = 0, c_st = 0, s_st = 0;
 
@@ -760,7 +833,7 @@ msd_wave_kernel(MsdLaunch p, NiceonlyLaunch c, u32 level0, StackNode *scratch, G
         wave_sync_global();  // popped before the pushes below reuse the slots
         u64 lo = p.start_lo, hi = p.start_hi;
         add_u128(lo, hi, nd.off);
-        const u32 act = lane < cnt ? classify_node(p, nd.depth, lo, hi, nd.size, g) : 0u;
+        const u32 act = lane < cnt ? classify_node<G, PairTab<G>::on>(p, nd.depth, lo, hi, nd.size, g, tab) : 0u;
         // a leaf: its stride descriptor to the queue (statistics as the
         // reference counts them: every MSD-surviving range)
         LeafDesc ld{0, 0, 0, 0};
@@ -770,9 +843,16 @@ msd_wave_kernel(MsdLaunch p, NiceonlyLaunch c, u32 level0, StackNode *scratch, G
             c_st += ld.count;
             s_st += nd.size;
         }
+#ifdef NICE_PROBES
+        const bool put = act == 1 && ld.count != 0 && !(p.probe & 4);  // probe 4: MSD only
+#else
         const bool put = act == 1 && ld.count != 0;
+#endif
         const u64 bl = __ballot(put);
-        if (put) q[(lq_tail + lane_rank(bl)) & (kLeafQ - 1)] = Leaf{ld.b0_lo, ld.b0_hi, ld.g0, (u32)ld.count};
+        if (put) {
+            if constexpr (WALK) qw[(lq_tail + lane_rank(bl)) & (kWalkQ - 1)] = LeafW{ld.b0_lo, ld.g0, (u32)ld.count};
+            else q[(lq_tail + lane_rank(bl)) & (kLeafQ - 1)] = Leaf{ld.b0_lo, ld.b0_hi, ld.g0, (u32)ld.count};
+        }
         lq_tail += (u32)__popcll(bl);
         // a split: both halves on the stack, one level deeper
         const u64 bs = __ballot(act == 2);
@@ -788,8 +868,14 @@ msd_wave_kernel(MsdLaunch p, NiceonlyLaunch c, u32 level0, StackNode *scratch, G
             sp += 2 * nsplit;
         }
         wave_sync_global();
-        // test queued leaves 64 at a time
-        if (lq_tail - lq_head >= 64) {
+        // test queued leaves: the lane walk once kWalkAt are queued, else 64
+        // at a time in packed groups
+        if constexpr (WALK) {
+            if (lq_tail - lq_head >= kWalkAt) {
+                walk_leaves<IsConst<G>::base>(c, qw, lq_head, lq_tail - lq_head, lane, cw);
+                lq_head = lq_tail;
+            }
+        } else if (lq_tail - lq_head >= 64) {
             wave_sync_lds();
             for (u32 gq = 0; gq < 64; gq += kLeafGroup) {
                 Leaf lf{0, 0, 0, 0};
@@ -800,6 +886,10 @@ msd_wave_kernel(MsdLaunch p, NiceonlyLaunch c, u32 level0, StackNode *scratch, G
         }
     }
     wave_sync_lds();
+    if constexpr (WALK) {
+        if (lq_head != lq_tail) walk_leaves<IsConst<G>::base>(c, qw, lq_head, lq_tail - lq_head, lane, cw);
+        lq_head = lq_tail;
+    }
     while (lq_head != lq_tail) {
         const u32 n = lq_tail - lq_head < kLeafGroup ? lq_tail - lq_head : kLeafGroup;
         Leaf lf{0, 0, 0, 0};

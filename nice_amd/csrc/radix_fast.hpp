@@ -315,9 +315,46 @@ __host__ __device__ __forceinline__ void msd_prefix(const u32 (&F)[N], const u32
     }
 }
 
+// msd_prefix for two-word bases with the LDS pair-mask table: per limb one
+// table read and a few selects instead of a test-and-set per digit; "a digit
+// repeats in the prefix" is "the prefix mask has fewer bits than the prefix
+// has digits".  The walk stops as soon as no lane of the wave is still inside
+// its common prefix.
+template <int BASE, int N>
+__device__ __forceinline__ void msd_prefix_tab(const u32 (&F)[N], const u32 (&L)[N], int D, u32 (&m)[2], u32 &dup,
+                                               const uint2 *tab) {
+    m[0] = m[1] = 0;
+    u32 nd = 0;
+    bool live = true;
+#pragma unroll
+    for (int t = N - 1; t >= 0; t--) {
+        if (!__builtin_amdgcn_ballot_w64(live)) break;  // wave-uniform
+        const u32 f = F[t], l = L[t];
+        const bool eq = live && f == l;
+        if (2 * t + 1 < D) {
+            const u32 fh = f / BASE, lh = l / BASE;
+            const bool heq = live && !eq && fh == lh;  // only the high digit is common
+            const uint2 e = tab[f];
+            const u64 hb = 1ull << fh;
+            m[0] |= eq ? e.x : (heq ? (u32)hb : 0u);
+            m[1] |= eq ? e.y : (heq ? (u32)(hb >> 32) : 0u);
+            nd += eq ? 2u : (heq ? 1u : 0u);
+        } else {  // the top limb of an odd digit count: one digit
+            const u64 b = 1ull << f;
+            m[0] |= eq ? (u32)b : 0u;
+            m[1] |= eq ? (u32)(b >> 32) : 0u;
+            nd += eq ? 1u : 0u;
+        }
+        live = eq;
+    }
+    dup = popc32(m[0]) + popc32(m[1]) != nd ? 1u : 0u;
+}
+
 // has_duplicate_msd_prefix on [first, last], both in range (equal digit counts).
-template <int BASE>
-__host__ __device__ __forceinline__ bool msd_skippable_fast(u64 f_lo, u64 f_hi, u64 l_lo, u64 l_hi) {
+// TAB: two-word bases with the LDS pair table `tab` (device only).
+template <int BASE, bool TAB = false>
+__host__ __device__ __forceinline__ bool msd_skippable_fast(u64 f_lo, u64 f_hi, u64 l_lo, u64 l_hi,
+                                                            const uint2 *tab = nullptr) {
     using R = Radix<BASE>;
     u32 Xf[R::NX], Xl[R::NX], Sf[R::NS], Sl[R::NS];
     to_limbs<BASE>(f_lo, f_hi, Xf);
@@ -325,13 +362,15 @@ __host__ __device__ __forceinline__ bool msd_skippable_fast(u64 f_lo, u64 f_hi, 
     square_limbs<BASE>(Xf, Sf);
     square_limbs<BASE>(Xl, Sl);
     u32 msq[R::MW], dsq;
-    msd_prefix<BASE>(Sf, Sl, R::D2, msq, dsq);
+    if constexpr (TAB) msd_prefix_tab<BASE>(Sf, Sl, R::D2, msq, dsq, tab);
+    else msd_prefix<BASE>(Sf, Sl, R::D2, msq, dsq);
     if (dsq) return true;
     u32 Cf[R::NC], Cl[R::NC];
     cube_limbs<BASE>(Sf, Xf, Cf);
     cube_limbs<BASE>(Sl, Xl, Cl);
     u32 mcu[R::MW], dcu;
-    msd_prefix<BASE>(Cf, Cl, R::D3, mcu, dcu);
+    if constexpr (TAB) msd_prefix_tab<BASE>(Cf, Cl, R::D3, mcu, dcu, tab);
+    else msd_prefix<BASE>(Cf, Cl, R::D3, mcu, dcu);
     if (dcu) return true;
     if (moverlap(msq, mcu)) return true;
     // Filter C (msd_prefix_filter.rs:461-559): first / b^2 == last / b^2, with
