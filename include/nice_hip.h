@@ -102,7 +102,9 @@ typedef struct {
     uint64_t range_numbers; /* numbers inside them */
     uint64_t candidates;    /* stride candidates checked on the GPU */
     uint32_t launches;
-    uint32_t reserved;
+    uint32_t square_ok;     /* device MSD, in-range fast bases: candidates whose square alone
+                               has no repeated digit (get_is_nice reached the cube scan),
+                               mod 2^32; 0 where not counted (host MSD, other bases) */
     double msd_seconds;     /* until the last MSD worker finished */
     double total_seconds;
 } nice_niceonly_stats;

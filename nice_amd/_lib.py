@@ -59,7 +59,7 @@ class nice_niceonly_opts(ctypes.Structure):
 class nice_niceonly_stats(ctypes.Structure):
     _fields_ = [("ranges", ctypes.c_uint64), ("range_numbers", ctypes.c_uint64),
                 ("candidates", ctypes.c_uint64), ("launches", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32), ("msd_seconds", ctypes.c_double),
+                ("square_ok", ctypes.c_uint32), ("msd_seconds", ctypes.c_double),
                 ("total_seconds", ctypes.c_double)]
 
 

@@ -108,6 +108,9 @@ class NiceonlyStats:
     launches: int
     msd_seconds: float
     total_seconds: float
+    # device MSD, in-range fast bases: candidates whose square alone has no
+    # repeated digit (mod 2^32; 0 where not counted)
+    square_ok: int = 0
 
 
 @dataclass
@@ -229,7 +232,7 @@ class GpuContext:
             check(rc)
             lst = [out[i].number_lo | (out[i].number_hi << 64) for i in range(n.value)]
             stats = NiceonlyStats(st.ranges, st.range_numbers, st.candidates, st.launches,
-                                  st.msd_seconds, st.total_seconds)
+                                  st.msd_seconds, st.total_seconds, st.square_ok)
             return lst, stats
 
     @staticmethod
@@ -261,7 +264,7 @@ class GpuContext:
             check(rc)
             return ([out[i].number_lo | (out[i].number_hi << 64) for i in range(n.value)],
                     NiceonlyStats(st.ranges, st.range_numbers, st.candidates, st.launches,
-                                  st.msd_seconds, st.total_seconds))
+                                  st.msd_seconds, st.total_seconds, st.square_ok))
 
     # -- both modes of one field ---------------------------------------------
     def both_raw(self, det_range, nice_range, base: int, **nice_opts):

@@ -119,8 +119,10 @@ struct MsdLaunch {
     MsdNode *q[2];                // ping-pong level queues
     uint32_t *counters;           // [0..23] level sizes, [24] leaf records (batch), [25]
                                   // overflow flag, [26] MSD-surviving ranges (sticky),
+                                  // [27] square survivors (written at the field's end),
                                   // [28..29] u64 candidates, [30..31] u64 numbers inside
-                                  // the ranges (sticky)
+                                  // the ranges (sticky); [32..95] square-survivor partial
+                                  // counts (workgroup b adds to 32 + b % 64, sticky)
     uint32_t q_cap;
     Leaf *leaves;
     uint32_t leaf_cap;
@@ -134,6 +136,7 @@ struct MsdLaunch {
     uint32_t probe;               // probe build only (NICE_MSD_PROBE): 1 no skip test, 2 no leaf stride math,
                                   // 4 wave kernel: no candidate test
 };
+constexpr uint32_t kMsdCounterWords = 96;
 // A leaf's candidate count is capped at kLeafPiece: longer runs are stored as
 // several leaves, so niceonly_kernel's per-wave sums of 8 leaves fit 32 bits.
 constexpr uint32_t kLeafPiece = 1u << 28;

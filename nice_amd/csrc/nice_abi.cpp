@@ -255,7 +255,7 @@ int ensure_desc(LeafBuf &b, uint32_t cap) {
 
 int ensure_msd(Slot &sl, uint32_t q_cap, uint32_t leaf_cap, uint64_t scratch_nodes, size_t wscratch_bytes = 0) {
     MsdBuf &m = sl.msd;
-    if (!m.counters) HIPCHK(hipMalloc(&m.counters, 32 * 4));
+    if (!m.counters) HIPCHK(hipMalloc(&m.counters, nice::kMsdCounterWords * 4));
     if (m.wscratch_bytes < wscratch_bytes) {
         HIPCHK(hipStreamSynchronize(sl.nstream));
         if (m.wscratch) HIPCHK(hipFree(m.wscratch));
@@ -1160,7 +1160,7 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
             if (i < nbatches) {
                 job.used[i] = 1;
                 if (d.slot[t].msd.dirty) {  // first use / after an interrupted field
-                    HIPCHK(hipMemsetAsync(d.slot[t].msd.counters, 0, 32 * 4, d.slot[t].nstream));
+                    HIPCHK(hipMemsetAsync(d.slot[t].msd.counters, 0, nice::kMsdCounterWords * 4, d.slot[t].nstream));
                     HIPCHK(hipMemsetAsync(d.slot[t].d_nice_count, 0, 4, d.slot[t].nstream));
                 }
                 d.slot[t].msd.dirty = true;  // until this field's epilogue is seen
@@ -1420,6 +1420,7 @@ int nice_niceonly_collect(nice_ctx *ctx, int t, nice_number *out, size_t cap, si
                     job.st.ranges += c[26];
                     job.st.candidates += cand;
                     job.st.range_numbers += nums;
+                    job.st.square_ok += c[27];
                 }
                 const uint32_t cnt = *sl.h_nice;
                 if (cnt > sl.nice.cap)

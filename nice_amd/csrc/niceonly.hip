@@ -192,6 +192,15 @@ __device__ __forceinline__ void cand_flush(const NiceonlyLaunch &p, CandWave &cw
     }
 }
 
+// This workgroup's square survivors (every wave's cube-queue total) into the
+// field's partial counts (counters[32 + b % 64]): one LDS add per wave, one
+// global add per workgroup.  Every thread calls it (a barrier inside).
+__device__ __forceinline__ void square_ok_flush(u32 *ctr, u32 *wg_sum, u32 waves_total, u32 lane) {
+    if (lane == 0 && waves_total) atomicAdd(wg_sum, waves_total);
+    __syncthreads();
+    if (threadIdx.x == 0 && ctr && *wg_sum) atomicAdd(&ctr[32 + blockIdx.x % 64], *wg_sum);
+}
+
 // End of a niceonly launch (every thread of the workgroup calls it): the last
 // workgroup to retire copies the field's results to mapped host memory (the
 // count is agent-atomic, so: own atomics drained, barrier, one agent add per
@@ -209,9 +218,17 @@ __device__ __forceinline__ void nice_launch_finish(const NiceFinish &fin, u32 *c
     u32 *ctr = fin.msd_counters;
     const u32 w = threadIdx.x;
     if (fin.count_mapped) {
-        if (ctr && w < 32) {
-            fin.msd_mapped[w] = __hip_atomic_load(&ctr[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (w >= 24) __hip_atomic_store(&ctr[w], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ctr && w < 64) {  // wave 0
+            // the square-survivor partials summed into word 27, then re-zeroed
+            u32 part = __hip_atomic_load(&ctr[32 + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctr[32 + w], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o);
+            if (w < 32) {
+                const u32 v = __hip_atomic_load(&ctr[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                fin.msd_mapped[w] = w == 27 ? part : v;
+                if (w >= 24) __hip_atomic_store(&ctr[w], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         if (w == 0) {
             *fin.count_mapped = __hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -232,7 +249,9 @@ niceonly_kernel(NiceonlyLaunch p, G g) {
     const u32 n_leaves = p.n_leaves_dev ? min(*p.n_leaves_dev, p.n_leaves) : p.n_leaves;
     __shared__ ulonglong2 cq[4][IsConst<G>::value ? kCubeQ : 1];
     __shared__ uint2 tab[PairTab<G>::N];
-    pair_tab_fill<G>(tab);
+    __shared__ u32 sq_sum;
+    if (threadIdx.x == 0) sq_sum = 0;
+    pair_tab_fill<G>(tab);  // (ends with a barrier)
     CandWave cw = cand_wave(p, cq[threadIdx.x >> 6], tab);
     // LPW leaves per wave (lanes >= LPW carry count 0): at the CPU path's
     // floor a leaf holds ~40 candidates, so 8 leaves keep a wave ~5 rounds
@@ -245,6 +264,7 @@ niceonly_kernel(NiceonlyLaunch p, G g) {
         check_leaf_group<G, LPW>(p, g, lf, lane, cw);
     }
     cand_flush<G>(p, cw, lane);
+    square_ok_flush(p.fin.msd_counters, &sq_sum, cw.q_tail, lane);
     if (p.fin.done) nice_launch_finish(p.fin, p.out.count);
 }
 
@@ -712,7 +732,8 @@ constexpr u32 kWaveWG = 512;
 // then the leaf's fields).  Queue entries are 16 bytes; the queue is walked
 // once it holds kWalkAt leaves (>= 3 per lane, so lanes rarely idle at the
 // end).  Massive field: 0.0688 -> 0.0652 s.  (Loading the next round's
-// residue ahead of the current test gained nothing: not latency-bound.)
+// residue ahead of the current test gained nothing, and stepping the limbs by
+// the residue gaps instead of converting n lost 7 %: 0.0696 s.)
 struct LeafW {
     u64 b0;
     u32 g0, count;
@@ -760,9 +781,10 @@ __device__ __forceinline__ void walk_leaves(const NiceonlyLaunch &c, const LeafW
             }
             have = --left != 0;
         }
+        const u64 nv_sq = nv;
         const u64 bal = __ballot(sq);
         if (bal) {
-            if (sq) cw.cq[(cw.q_tail + lane_rank(bal)) & (kCubeQ - 1)] = make_ulonglong2(nv, 0ull);
+            if (sq) cw.cq[(cw.q_tail + lane_rank(bal)) & (kCubeQ - 1)] = make_ulonglong2(nv_sq, 0ull);
             cw.q_tail += (u32)__popcll(bal);
             if (cw.q_tail - cw.q_head >= 64) {
                 cube_pass<B>(c, cw.cq, cw.q_head, 64, lane, cw.tab);
@@ -788,8 +810,10 @@ msd_wave_kernel(MsdLaunch p, NiceonlyLaunch c, u32 level0, StackNode *scratch, G
     __shared__ LeafW lw[W][WALK ? kWalkQ : 1];
     __shared__ uint2 tab[PairTab<G>::N];
     __shared__ unsigned long long stat[3];
+    __shared__ u32 sq_sum;
     if (threadIdx.x < 3) stat[threadIdx.x] = 0;
-    pair_tab_fill<G>(tab);
+    if (threadIdx.x == 0) sq_sum = 0;
+    pair_tab_fill<G>(tab);  // (ends with a barrier)
     const u32 lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const u64 gwave = (u64)blockIdx.x * W + wv, nwaves = (u64)gridDim.x * W;
     StackNode *st = scratch + gwave * kStackCap;
@@ -898,6 +922,7 @@ msd_wave_kernel(MsdLaunch p, NiceonlyLaunch c, u32 level0, StackNode *scratch, G
         lq_head += n;
     }
     cand_flush<G>(c, cw, lane);
+    square_ok_flush(c.fin.msd_counters, &sq_sum, cw.q_tail, lane);
     flush_stats(p, n_st, c_st, s_st, stat);
     if (c.fin.done) nice_launch_finish(c.fin, c.out.count);
 }

@@ -250,14 +250,19 @@ __host__ __device__ __forceinline__ bool is_nice_fast(u64 lo, u64 hi) {
 
 // The same two tests with the LDS pair table (two-word bases, see above).
 template <int BASE>
-__device__ __forceinline__ bool square_ok_tab(u64 lo, u64 hi, const uint2 *tab) {
+__device__ __forceinline__ bool square_ok_tab_limbs(const u32 (&X)[Radix<BASE>::NX], const uint2 *tab) {
     using R = Radix<BASE>;
     static_assert(R::MW == 2, "pair table: two-word bases");
-    u32 X[R::NX], S[R::NS];
-    to_limbs<BASE>(lo, hi, X);
+    u32 S[R::NS];
     square_limbs<BASE>(X, S);
     u32 m[2] = {0, 0};
     return limbs_popcount_tab<BASE>(S, R::D2, m, tab) == (u32)R::D2;
+}
+template <int BASE>
+__device__ __forceinline__ bool square_ok_tab(u64 lo, u64 hi, const uint2 *tab) {
+    u32 X[Radix<BASE>::NX];
+    to_limbs<BASE>(lo, hi, X);
+    return square_ok_tab_limbs<BASE>(X, tab);
 }
 template <int BASE>
 __device__ __forceinline__ bool is_nice_tab(u64 lo, u64 hi, const uint2 *tab) {

@@ -236,8 +236,9 @@ static inline u32 nud(u128 n, u32 base) {
 
 u32 oracle_num_unique_digits(u64 lo, u64 hi, u32 base) { return nud(mk(lo, hi), base); }
 
-/* client_process.rs:222-413 */
-static inline __attribute__((always_inline)) int is_nice_impl(u128 n, u32 base) {
+/* client_process.rs:222-413.  sq_ok (test statistic, may be NULL): set to 1
+ * when n^2 alone has no repeated digit, i.e. the scan reached the cube. */
+static inline __attribute__((always_inline)) int is_nice_impl2(u128 n, u32 base, int *sq_ok) {
     big t, sq, cu;
     big_set(&t, n);
     big_mul_u128(&t, n, &sq);
@@ -250,6 +251,7 @@ static inline __attribute__((always_inline)) int is_nice_impl(u128 n, u32 base) 
         if (*w & bit) return 0;
         *w |= bit;
     }
+    if (sq_ok) *sq_ok = 1;
     big_mul_u128(&sq, n, &cu);
     while (cu.top >= 0) {
         u32 d = big_divrem(&cu, base);
@@ -259,6 +261,9 @@ static inline __attribute__((always_inline)) int is_nice_impl(u128 n, u32 base) 
         *w |= bit;
     }
     return 1;
+}
+static inline __attribute__((always_inline)) int is_nice_impl(u128 n, u32 base) {
+    return is_nice_impl2(n, base, NULL);
 }
 static int isn_10(u128 n) { return is_nice_impl(n, 10); }
 static int isn_40(u128 n) { return is_nice_impl(n, 40); }
@@ -385,10 +390,12 @@ typedef struct {
     u64 *stride_res; u64 stride_count; u64 stride_mod;
     u64 *cand_counts;
     u64 *range_counts;
+    u64 *sq_counts; /* test statistic: candidates whose square has no repeat (or NULL) */
 } job;
 
 static uint64_t niceonly_range_impl(u128 s, u128 e, u32 base, const u64 *res, u64 R,
-                                    u64 M, u64 floor_size, misslist *out, u64 *n_ranges);
+                                    u64 M, u64 floor_size, misslist *out, u64 *n_ranges,
+                                    u64 *n_sq);
 
 static void *worker(void *arg) {
     job *j = (job *)arg;
@@ -403,7 +410,8 @@ static void *worker(void *arg) {
             j->cand_counts[i] = niceonly_range_impl(s, e, j->base, j->stride_res,
                                                     j->stride_count, j->stride_mod,
                                                     j->floor_size, &j->lists[i],
-                                                    &j->range_counts[i]);
+                                                    &j->range_counts[i],
+                                                    j->sq_counts ? &j->sq_counts[i] : NULL);
         }
     }
     return NULL;
@@ -644,8 +652,10 @@ u64 oracle_valid_ranges(u64 slo, u64 shi, u64 elo, u64 ehi, u32 base, u64 floor_
 
 /* client_process.rs:439-465 + stride_filter.rs:139-155 */
 static uint64_t niceonly_range_impl(u128 s, u128 e, u32 base, const u64 *res, u64 R,
-                                    u64 M, u64 floor_size, misslist *out, u64 *n_ranges) {
+                                    u64 M, u64 floor_size, misslist *out, u64 *n_ranges,
+                                    u64 *n_sq) {
     if (n_ranges) *n_ranges = 0;
+    if (n_sq) *n_sq = 0;
     if (R == 0) return 0;
     rangelist rl = {0};
     valid_ranges_rec(s, e, base, 0, 22, floor_size, 2, &rl);
@@ -656,7 +666,15 @@ static uint64_t niceonly_range_impl(u128 s, u128 e, u32 base, const u64 *res, u6
         u128 n = first_valid_at_or_after(res, R, M, rl.s[q], &idx);
         while (n < rl.e[q]) {
             cands++;
-            if (is_nice(n, base)) ml_push(out, n, base);
+            int nice;
+            if (n_sq) {
+                int sq_ok = 0;
+                nice = is_nice_impl2(n, base, &sq_ok);
+                *n_sq += (u64)sq_ok;
+            } else {
+                nice = is_nice(n, base);
+            }
+            if (nice) ml_push(out, n, base);
             n += (idx + 1 < R) ? res[idx + 1] - res[idx] : M - res[idx] + res[0];
             idx = (idx + 1) % R;
         }
@@ -687,7 +705,7 @@ u64 oracle_process_range_niceonly(u64 slo, u64 shi, u64 elo, u64 ehi, u32 base, 
     u64 *res = stride_table_alloc(base, k, &R, &M);
     misslist ml = {0};
     u64 c = niceonly_range_impl(mk(slo, shi), mk(elo, ehi), base, res, R, M, floor_size, &ml,
-                                NULL);
+                                NULL, NULL);
     if (n_candidates) *n_candidates = c;
     u64 n = emit_nice(&ml, out, cap);
     free(ml.n); free(ml.u); free(res);
@@ -699,9 +717,24 @@ u64 oracle_process_range_niceonly(u64 slo, u64 shi, u64 elo, u64 ehi, u32 base, 
  * processed on that field's chunk grid when it starts on a grid point.
  * *n_ranges receives the number of MSD-surviving ranges (get_valid_ranges
  * output length summed over chunks, msd_prefix_filter.rs:665-674). */
+u64 oracle_process_field_niceonly_sq(u64 slo, u64 shi, u64 elo, u64 ehi, u32 base,
+                                     int threads, u64 chunk, u64 floor_size, u64 *out,
+                                     u64 cap, u64 *n_candidates, u64 *n_ranges, u64 *n_sq);
+
 u64 oracle_process_field_niceonly_ex(u64 slo, u64 shi, u64 elo, u64 ehi, u32 base,
                                      int threads, u64 chunk, u64 floor_size, u64 *out,
                                      u64 cap, u64 *n_candidates, u64 *n_ranges) {
+    return oracle_process_field_niceonly_sq(slo, shi, elo, ehi, base, threads, chunk, floor_size,
+                                            out, cap, n_candidates, n_ranges, NULL);
+}
+
+/* _ex plus the test statistic *n_sq: stride candidates whose square alone has
+ * no repeated digit (get_is_nice reached the cube scan).  The GPU's in-range
+ * test counts the same set (its square-survivor queue), which pins the
+ * candidate enumeration and the digit test even where no number is nice. */
+u64 oracle_process_field_niceonly_sq(u64 slo, u64 shi, u64 elo, u64 ehi, u32 base,
+                                     int threads, u64 chunk, u64 floor_size, u64 *out,
+                                     u64 cap, u64 *n_candidates, u64 *n_ranges, u64 *n_sq) {
     job j;
     memset(&j, 0, sizeof(j));
     j.start = mk(slo, shi); j.end = mk(elo, ehi); j.base = base; j.mode = 1;
@@ -713,20 +746,24 @@ u64 oracle_process_field_niceonly_ex(u64 slo, u64 shi, u64 elo, u64 ehi, u32 bas
     j.lists = calloc(j.nchunks, sizeof(misslist));
     j.cand_counts = calloc(j.nchunks, sizeof(u64));
     j.range_counts = calloc(j.nchunks, sizeof(u64));
+    j.sq_counts = n_sq ? calloc(j.nchunks, sizeof(u64)) : NULL;
     run_job(&j, threads);
     misslist all = {0};
-    u64 cands = 0, ranges = 0;
+    u64 cands = 0, ranges = 0, sqs = 0;
     for (u64 i = 0; i < j.nchunks; i++) {
         for (size_t q = 0; q < j.lists[i].len; q++)
             ml_push(&all, mk(j.lists[i].n[2 * q], j.lists[i].n[2 * q + 1]), base);
         cands += j.cand_counts[i];
         ranges += j.range_counts[i];
+        if (j.sq_counts) sqs += j.sq_counts[i];
         free(j.lists[i].n); free(j.lists[i].u);
     }
     if (n_candidates) *n_candidates = cands;
     if (n_ranges) *n_ranges = ranges;
+    if (n_sq) *n_sq = sqs;
     u64 n = emit_nice(&all, out, cap);
     free(all.n); free(all.u); free(j.lists); free(j.cand_counts); free(j.range_counts);
+    free(j.sq_counts);
     free(j.stride_res);
     return n;
 }

@@ -118,6 +118,13 @@ uint64_t oracle_process_field_niceonly_ex(uint64_t start_lo, uint64_t start_hi,
                                           int threads, uint64_t chunk, uint64_t floor_size,
                                           uint64_t *out, uint64_t cap, uint64_t *n_candidates,
                                           uint64_t *n_ranges);
+/* _ex plus *n_sq: candidates whose square alone has no repeated digit (test
+ * statistic pinning the GPU's square-survivor count). */
+uint64_t oracle_process_field_niceonly_sq(uint64_t start_lo, uint64_t start_hi,
+                                          uint64_t end_lo, uint64_t end_hi, uint32_t base,
+                                          int threads, uint64_t chunk, uint64_t floor_size,
+                                          uint64_t *out, uint64_t cap, uint64_t *n_candidates,
+                                          uint64_t *n_ranges, uint64_t *n_sq);
 
 #ifdef __cplusplus
 }

@@ -70,6 +70,9 @@ def lib():
         L.oracle_process_field_niceonly_ex.argtypes = [u64, u64, u64, u64, u32, i32, u64, u64,
                                                        P64, u64, P64, P64]
         L.oracle_process_field_niceonly_ex.restype = u64
+        L.oracle_process_field_niceonly_sq.argtypes = [u64, u64, u64, u64, u32, i32, u64, u64,
+                                                       P64, u64, P64, P64, P64]
+        L.oracle_process_field_niceonly_sq.restype = u64
         _lib = L
     return _lib
 
@@ -213,3 +216,19 @@ def process_field_niceonly_ex(start: int, end: int, base: int, threads: int, chu
         raise OverflowError("nice list exceeded capacity")
     nice = [(buf[2 * i] | (buf[2 * i + 1] << 64), base) for i in range(n)]
     return FieldResults([], nice), cands.value, ranges.value
+
+
+def process_field_niceonly_sq(start: int, end: int, base: int, threads: int, chunk: int = 0,
+                              floor_size: int = 0, cap: int = 1 << 16):
+    """process_field_niceonly_ex plus the number of stride candidates whose
+    square alone has no repeated digit (get_is_nice reached the cube scan): a
+    test statistic for the GPU's square-survivor count.  Returns
+    (FieldResults, candidates, ranges, square_ok)."""
+    buf = (ctypes.c_uint64 * (2 * cap))()
+    cands, ranges, sq = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    n = lib().oracle_process_field_niceonly_sq(*_split(start), *_split(end), base, threads, chunk,
+                                               floor_size, buf, cap, cands, ranges, sq)
+    if n > cap:
+        raise OverflowError("nice list exceeded capacity")
+    nice = [(buf[2 * i] | (buf[2 * i + 1] << 64), base) for i in range(n)]
+    return FieldResults([], nice), cands.value, ranges.value, sq.value

@@ -565,6 +565,34 @@ def test_massive_windows_with_candidates(ctx, where):
         assert [str(n) for n in lst] == x["nice_numbers"]
 
 
+def test_square_survivors_match_oracle(ctx):
+    """No nice number is known at these bases, so a wrong digit test or a
+    wrong candidate enumeration would pass every nice-list comparison.  This
+    pins both: the number of stride candidates whose square alone has no
+    repeated digit (the device's square-survivor queue; the oracle's
+    get_is_nice reaching the cube scan) must match, with candidates and ranges,
+    on
+      * the b40 1e9 field (fused per-chunk MSD + candidate kernel),
+      * a 64-chunk window of the massive b50 field where its candidates are
+        (level BFS to the root level, then the wave kernel's own recursion,
+        lane walk, stepped limbs),
+      * 1e9 windows of the live bases 52 / 53 on 1e8 chunks (wave kernel)."""
+    m = _massive()
+    s50 = int(m["start"])
+    s40 = O.base_range(40)[0]
+    cases = [(s40, s40 + 10 ** 9, 40, 0), (s50 + 8 * 10 ** 12, s50 + 8 * 10 ** 12 + 64 * 10 ** 8, 50, 10 ** 8)]
+    for b in (52, 53):
+        lo, hi = O.base_range(b)
+        a = lo + (hi - lo) // 3
+        cases.append((a, a + 10 ** 9, b, 10 ** 8))
+    for a, e, b, chunk in cases:
+        res, cands, ranges, sq = O.process_field_niceonly_sq(a, e, b, 16, chunk)
+        lst, st = ctx.niceonly_raw(a, e, b, chunk_size=chunk, msd_where="device")
+        assert (st.candidates, st.ranges, st.square_ok) == (cands, ranges, sq), (b, a)
+        assert lst == [n for n, _ in res.nice_numbers]
+        assert sq > 0
+
+
 def test_massive_whole_field_sums():
     """The whole 1e13 field on the device MSD: totals equal the sum of the
     oracle windows (7 480 186 005 candidates, 166 585 582 ranges, no nice

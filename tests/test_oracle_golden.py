@@ -147,6 +147,39 @@ def test_mt_driver_matches_single():
     assert r1 == r2 and r1.nice_numbers == [(69, 10)]
 
 
+def _digits(v, b):
+    out = []
+    while v:
+        v, d = divmod(v, b)
+        out.append(d)
+    return out
+
+
+def test_square_survivor_statistic():
+    """oracle_process_field_niceonly_sq's test statistic (candidates whose
+    square alone has no repeated digit) restated in Python on a b40 window
+    with MSD survivors: walk the oracle's valid ranges with the stride
+    residues and test n^2's digits directly."""
+    s, _ = O.base_range(40)
+    a = s + 10 ** 9 - 3 * 10 ** 6          # inside the extra-large field, ranges survive
+    e = a + 2 * 10 ** 6
+    res, cands, ranges, sq = O.process_field_niceonly_sq(a, e, 40, 4, 10 ** 6)
+    M, residues = O.stride_residues(40, 2)
+    want_c = want_sq = want_r = 0
+    for c0 in range(a, e, 10 ** 6):
+        for lo, hi in O.valid_ranges(c0, min(c0 + 10 ** 6, e), 40):
+            want_r += 1
+            for base_ in range(lo - lo % M, hi, M):
+                for r in residues:
+                    n = base_ + r
+                    if lo <= n < hi:
+                        want_c += 1
+                        d = _digits(n * n, 40)
+                        want_sq += len(set(d)) == len(d)
+    assert (cands, ranges, sq) == (want_c, want_r, want_sq)
+    assert want_c > 1000 and 0 < want_sq < want_c
+
+
 def test_scan_depth_consistent():
     # scan depth == total digits iff is_nice (no repeat anywhere)
     s, _ = O.base_range(40)
