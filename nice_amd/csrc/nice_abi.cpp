@@ -1137,7 +1137,9 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
             while (last < 22 && ((cnk + (1ull << last) - 1) >> last) >= 2 * fl) last++;
             while (wlevel < last && ((cnk + (1ull << wlevel) - 1) >> wlevel) > (1ull << 26)) wlevel++;
             for (;;) {
-                cpb = std::min<uint64_t>(mine, std::max<uint64_t>(1, (1ull << 24) >> wlevel));
+                // (a multi-device context gets at least one batch per device)
+                const uint64_t per_dev = (mine + ctx->devs.size() - 1) / ctx->devs.size();
+                cpb = std::min<uint64_t>(per_dev, std::max<uint64_t>(1, (1ull << 24) >> wlevel));
                 if ((cpb << wlevel) >= target || wlevel >= last) break;
                 wlevel++;
             }

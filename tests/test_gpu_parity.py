@@ -316,6 +316,14 @@ def test_niceonly_multi_device_context():
         one, st1 = N.GpuContext([0]).niceonly_raw(s, s + 3 * 10 ** 8, 40, msd_where=where,
                                                   chunk_size=10 ** 6, msd_floor=4)
         assert lst == one and st.candidates == st1.candidates
+        assert (st.ranges, st.square_ok) == (st1.ranges, st1.square_ok)
+    # the wave path on a massive window with candidates: one batch per device
+    a = int(_massive()["start"]) + 8 * 10 ** 12
+    lst, st = c.niceonly_raw(a, a + 16 * 10 ** 8, 50, chunk_size=10 ** 8, msd_where="device")
+    one, st1 = N.GpuContext([0]).niceonly_raw(a, a + 16 * 10 ** 8, 50, chunk_size=10 ** 8,
+                                              msd_where="device")
+    assert lst == one and st.square_ok > 0 and st.launches == 2
+    assert (st.candidates, st.ranges, st.square_ok) == (st1.candidates, st1.ranges, st1.square_ok)
     c.close()
 
 
