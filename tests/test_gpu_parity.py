@@ -601,6 +601,28 @@ def test_square_survivors_match_oracle(ctx):
         assert sq > 0
 
 
+def test_wave_path_other_bases(ctx):
+    """The wave kernel (large chunks) beyond the lane walk: the packed
+    candidate groups with a VALU digit decode (b80, three-word masks), the
+    generic kernels (b45, b62: no compile-time base), and the out-of-range
+    path (b10 [47, 100): generic MSD test inside the wave kernel, must find
+    69).  Candidates, ranges and nice lists against the oracle at 1e8 chunks
+    (square survivors too where the in-range fast path counts them)."""
+    cases = [(47, 100, 10)]
+    for b, fr, size in ((80, 0.9, 10 ** 10), (45, 0.5, 10 ** 9), (62, 0.5, 10 ** 9)):
+        s, e = O.base_range(b)
+        a = s + int((e - s) * fr)
+        cases.append((a, a + size, b))
+    for a, e, b in cases:
+        res, cands, ranges, sq = O.process_field_niceonly_sq(a, e, b, 16, 10 ** 8)
+        lst, st = ctx.niceonly_raw(a, e, b, chunk_size=10 ** 8, msd_where="device")
+        assert (st.candidates, st.ranges) == (cands, ranges), (b, a)
+        assert lst == [n for n, _ in res.nice_numbers], (b, a)
+        if b == 80:
+            assert st.square_ok == sq > 0
+    assert ctx.niceonly_raw(47, 100, 10, chunk_size=10 ** 8, msd_where="device")[0] == [69]
+
+
 def test_massive_whole_field_sums():
     """The whole 1e13 field on the device MSD: totals equal the sum of the
     oracle windows (7 480 186 005 candidates, 166 585 582 ranges, no nice
