@@ -158,9 +158,9 @@ hipError_t launch_msd_device(const MsdLaunch &p, int num_cus, hipStream_t s, Chu
 // enough roots to fill the chip), then msd_wave_kernel: the recursion below
 // level0 AND the candidate test of every leaf in one launch (`c` holds the
 // residues, output and finish; its leaf fields are unused), `grid` workgroups
-// of 4 waves, each wave with a kStackCap-node stack in `scratch`
-// (msd_wave_scratch_bytes(grid)).  Leaves of the BFS levels go to p.leaves
-// and are tested by the same launch.
+// of msd_wave_waves_per_group() waves, each wave with a kStackCap-node stack
+// in `scratch` (msd_wave_scratch_bytes(grid)).  Leaves of the BFS levels go
+// to p.leaves and are tested by the same launch.
 hipError_t launch_msd_wave(const MsdLaunch &p, const NiceonlyLaunch &c, uint32_t level0, void *scratch,
                            uint32_t grid, int num_cus, hipStream_t s);
 size_t msd_wave_scratch_bytes(uint32_t grid);

@@ -5,19 +5,24 @@
 // optionally, the host MSD recursion in front of it
 // (common/src/msd_prefix_filter.rs:382-674).
 //
-// niceonly_kernel: wave-level load balancing.  A wave takes 64 leaves (one per
-// lane), scans their candidate counts across the wave, and then walks the
-// packed candidate space 64 at a time: lane k finds its leaf by a 6-step
-// binary search over the wave's exclusive prefix (cross-lane reads, no LDS),
-// rebuilds n = b0 + ((g0 + j) / R) * M + residues[(g0 + j) % R] and runs the
-// reference's early-exit check (client_process.rs:222-253).  A leaf holds ~20
-// candidates at the CPU path's MSD floor of 250 (b40), so one-wave-per-range
-// would leave two thirds of a 64-lane wave idle.
+// niceonly_kernel: wave-level load balancing.  A wave takes 8 leaves (lanes
+// 0..7), scans their candidate counts across the wave, and then walks the
+// packed candidate space 64 at a time: lane k finds its leaf by a binary
+// search over the wave's exclusive prefix (cross-lane reads), rebuilds n = b0
+// + ((g0 + j) / R) * M + residues[(g0 + j) % R] and tests it: in range, the
+// digit union of n^2 (pair-mask table in LDS) and, for the few repeat-free
+// squares queued per wave, of n^3 has b members (client_process.rs:222-253).
+// A leaf holds ~20 candidates at the CPU path's MSD floor of 250 (b40), so
+// one-wave-per-range would leave two thirds of a 64-lane wave idle.
 //
+// msd_fused_kernel: a chunk's whole MSD recursion in one workgroup (chunks up
+// to 16384 floors, e.g. the client's 1e6 chunks).
 // msd_level_kernel: the MSD recursion as a level-synchronous BFS.  Every node
 // of level d is one lane: leaf -> stride-index descriptor appended to the leaf
-// list; skippable -> dropped; else two children appended to level d+1.  The
-// recursion is depth-limited (22), so 23 launches per batch, no host sync.
+// list; skippable -> dropped; else two children appended to level d+1.
+// msd_wave_kernel: larger chunks -- the level BFS stops at a root level and
+// each wave recurses below it with its own work stack, testing the leaves it
+// finds in the same launch (see there).
 #include "kernels.h"
 #include "nice_device.hpp"
 #include "radix_fast.hpp"
