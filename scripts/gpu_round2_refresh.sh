@@ -15,3 +15,4 @@ timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_o
 timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write -o p -- python3 $R/scripts/prof_detailed.py 2 > $R/gpurun_out/pmc_write.log 2>&1
 cd $R
 timeout -k 10 300 python3 -u scripts/bench_configs.py > gpurun_out/configs.jsonl 2> gpurun_out/configs.err
+timeout -k 10 300 python3 -u scripts/massive_deal.py 8 3 > gpurun_out/massive_deal_8.log 2>&1
