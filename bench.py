@@ -34,6 +34,7 @@ Timing: barrier + device sync on both sides of exactly K steps, max over ranks.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -114,15 +115,26 @@ def rank_field(base_start: int, rank: int, size: int = FIELD_SIZE):
 def timed(step, steps: int, sync, dist=None, tail=None):
     """Barrier + device sync on both sides of exactly `steps` steps (plus
     `tail`, e.g. collecting the pipeline's last fields); returns the max
-    elapsed seconds over ranks (all_reduce MAX)."""
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    if tail is not None:
-        tail()
-    sync()
-    elapsed = time.perf_counter() - t0
+    elapsed seconds over ranks (all_reduce MAX).  Python's cyclic garbage
+    collector is paused inside the region (as timeit does): a collection
+    pass over the interpreter's objects stalls the host that feeds the
+    pipeline, and at a strong-scaling shard's ~0.25 ms per step one such
+    stall is several steps' worth of GPU time."""
+    gc.collect()
+    gc_was = gc.isenabled()
+    gc.disable()
+    try:
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        if tail is not None:
+            tail()
+        sync()
+        elapsed = time.perf_counter() - t0
+    finally:
+        if gc_was:
+            gc.enable()
     if dist is not None:
         import torch
         dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
