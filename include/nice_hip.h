@@ -35,6 +35,8 @@ extern "C" {
 #define NICE_ERR_HIP 2         /* HIP runtime / kernel failure */
 #define NICE_ERR_CAPACITY 3    /* caller's output list too small; *n_out = needed */
 #define NICE_ERR_NO_DEVICE 4   /* no usable GPU */
+#define NICE_ERR_MSD_OVERFLOW 5 /* device MSD work queues overflowed (msd_floor too small for
+                                   chunk_size); not retryable with a larger list */
 
 /* NiceNumberSimple (common/src/lib.rs:182-186). */
 typedef struct {

@@ -18,6 +18,7 @@ NICE_ERR_INVALID = 1
 NICE_ERR_HIP = 2
 NICE_ERR_CAPACITY = 3
 NICE_ERR_NO_DEVICE = 4
+NICE_ERR_MSD_OVERFLOW = 5
 
 # Every symbol include/nice_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = (

@@ -177,7 +177,7 @@ class GpuContext:
             n = ctypes.c_size_t()
             rc = lib().nice_process_range_detailed(self._h, *_split(start), *_split(end), base,
                                                    hist, out, cap, n)
-            if rc == _lib.NICE_ERR_CAPACITY:
+            if rc == _lib.NICE_ERR_CAPACITY and n.value > cap:  # retry only with more room
                 cap = n.value
                 continue
             check(rc)
@@ -202,7 +202,7 @@ class GpuContext:
             out = self._out_buf(cap)
             n = ctypes.c_size_t()
             rc = lib().nice_detailed_collect(self._h, ticket, hist, out, cap, n)
-            if rc == _lib.NICE_ERR_CAPACITY:
+            if rc == _lib.NICE_ERR_CAPACITY and n.value > cap:  # retry only with more room
                 cap = n.value
                 continue
             check(rc)
@@ -226,7 +226,7 @@ class GpuContext:
             n = ctypes.c_size_t()
             rc = lib().nice_process_range_niceonly_ex(self._h, *_split(start), *_split(end), base,
                                                       opts, out, cap, n, st)
-            if rc == _lib.NICE_ERR_CAPACITY:
+            if rc == _lib.NICE_ERR_CAPACITY and n.value > cap:  # retry only with more room
                 cap = n.value
                 continue
             check(rc)
@@ -258,7 +258,7 @@ class GpuContext:
             out = self._out_buf(cap)
             n = ctypes.c_size_t()
             rc = lib().nice_niceonly_collect(self._h, ticket, out, cap, n, st)
-            if rc == _lib.NICE_ERR_CAPACITY:
+            if rc == _lib.NICE_ERR_CAPACITY and n.value > cap:  # retry only with more room
                 cap = n.value
                 continue
             check(rc)
@@ -444,7 +444,7 @@ def process_range_detailed_cpu(range_: FieldSize, base: int, threads: int = 1) -
         out, n = _cpu_out(cap), ctypes.c_size_t()
         rc = lib().nice_cpu_process_range_detailed(*_split(range_.range_start), *_split(range_.range_end),
                                                     base, threads, hist, out, cap, n)
-        if rc == _lib.NICE_ERR_CAPACITY:
+        if rc == _lib.NICE_ERR_CAPACITY and n.value > cap:  # retry only with more room
             cap = n.value
             continue
         check(rc)
@@ -467,7 +467,7 @@ def process_range_niceonly_cpu(range_: FieldSize, base: int,
         out, n = _cpu_out(cap), ctypes.c_size_t()
         rc = lib().nice_cpu_process_range_niceonly(*_split(range_.range_start), *_split(range_.range_end),
                                                     base, k, threads, out, cap, n)
-        if rc == _lib.NICE_ERR_CAPACITY:
+        if rc == _lib.NICE_ERR_CAPACITY and n.value > cap:  # retry only with more room
             cap = n.value
             continue
         check(rc)

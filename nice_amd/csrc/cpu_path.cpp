@@ -69,7 +69,10 @@ bool is_nice(u128 n, const BP &bp) {
     nice::digits_of(cu, 12, bp, d);
     for (int i = 0; i < d.n; i++)
         if (!s.add(d.d[i])) return false;
-    return s.count() == bp.b;
+    // No digit-count test: the reference's get_is_nice returns true once both
+    // scans finish without a repeat (client_process.rs:258-290), so below a
+    // base's valid range an n whose digits are merely distinct is listed.
+    return true;
 }
 
 struct Piece {

@@ -164,6 +164,9 @@ struct Device {
     int id = 0;
     int num_cus = 0;
     hipStream_t aux = nullptr;    // self-check recomputes (never behind a queued field); lazily created
+    uint64_t *chk_n = nullptr;    // self-check recompute buffers, grown on demand (a hipFree per
+    uint32_t *chk_u = nullptr;    // collect would synchronise the whole device)
+    size_t chk_cap = 0;
     Slot slot[kSlots];
     std::map<uint32_t, uint32_t *> residues;  // base*8+k -> device residue table
     std::map<uint32_t, uint32_t *> ranks;     // base*8+k -> lower_bound(residues, r), r in [0, M]
@@ -224,6 +227,19 @@ struct nice_ctx {
 };
 
 namespace {
+
+// The slot a new field takes: the round-robin position if it is free (so
+// consecutive fields alternate slots), else the next free one after it
+// (tickets may be collected in any order).  -1 if every slot is in flight.
+template <class Job>
+int free_slot(const Job *jobs, int next) {
+    const int n = slots_used();
+    for (int i = 0; i < n; i++) {
+        const int t = (next + i) % n;
+        if (!jobs[t].active) return t;
+    }
+    return -1;
+}
 
 int ensure_listbuf(Device &d, ListBuf &l, uint32_t cap, bool with_u) {
     if (l.cap >= cap) return NICE_OK;
@@ -367,6 +383,8 @@ void device_free(Device &d) {
         for (hipEvent_t ev : {sl.ev0, sl.ev1, sl.ev_done, sl.nice_done})
             if (ev) (void)hipEventDestroy(ev);
     }
+    if (d.chk_n) (void)hipFree(d.chk_n);
+    if (d.chk_u) (void)hipFree(d.chk_u);
     if (d.aux) (void)hipStreamDestroy(d.aux);
     for (auto &sl : d.slot) sl.stream = nullptr;
 }
@@ -561,10 +579,10 @@ int enqueue_detailed_shard(Device &d, Slot &sl, u128 s, u128 e, uint32_t base) {
 }
 
 int detailed_submit(nice_ctx *ctx, u128 s, u128 e, uint32_t base, int *ticket) {
-    const int t = ctx->det_next;
-    DetJob &job = ctx->det[t];
-    if (job.active)
+    const int t = free_slot(ctx->det, ctx->det_next);
+    if (t < 0)
         return fail(NICE_ERR_INVALID, "three detailed fields already in flight on this context; collect one first");
+    DetJob &job = ctx->det[t];
     const size_t nd = ctx->devs.size();
     const u128 size = e - s;
     // Shard bounds: contiguous, in device order (ascending n).
@@ -653,17 +671,24 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
             pairs[2 * i] = lo64(job.all[i].n);
             pairs[2 * i + 1] = hi64(job.all[i].n);
         }
-        uint64_t *dn = nullptr;
-        uint32_t *du = nullptr;
-        HIPCHK(hipMalloc(&dn, n * 16));
-        HIPCHK(hipMalloc(&du, n * 4));
+        if (d.chk_cap < n) {
+            // grown rarely (the recompute of the previous field finished
+            // before its collect returned, so nothing reads the old buffers)
+            if (d.chk_n) HIPCHK(hipFree(d.chk_n));
+            if (d.chk_u) HIPCHK(hipFree(d.chk_u));
+            d.chk_n = nullptr;
+            d.chk_u = nullptr;
+            d.chk_cap = 0;
+            const size_t c = std::max<size_t>(n, 4096);
+            HIPCHK(hipMalloc(&d.chk_n, c * 16));
+            HIPCHK(hipMalloc(&d.chk_u, c * 4));
+            d.chk_cap = c;
+        }
         std::vector<uint32_t> u(n);
-        hipError_t err = hipMemcpyAsync(dn, pairs.data(), n * 16, hipMemcpyHostToDevice, d.aux);
-        if (err == hipSuccess) err = nice::launch_unique_counts(dn, (uint32_t)n, base, du, d.aux);
-        if (err == hipSuccess) err = hipMemcpyAsync(u.data(), du, n * 4, hipMemcpyDeviceToHost, d.aux);
+        hipError_t err = hipMemcpyAsync(d.chk_n, pairs.data(), n * 16, hipMemcpyHostToDevice, d.aux);
+        if (err == hipSuccess) err = nice::launch_unique_counts(d.chk_n, (uint32_t)n, base, d.chk_u, d.aux);
+        if (err == hipSuccess) err = hipMemcpyAsync(u.data(), d.chk_u, n * 4, hipMemcpyDeviceToHost, d.aux);
         if (err == hipSuccess) err = hipStreamSynchronize(d.aux);
-        (void)hipFree(dn);
-        (void)hipFree(du);
         if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("self-check: ") + hipGetErrorString(err));
         for (size_t i = 0; i < n; i++)
             if (u[i] != job.all[i].u)
@@ -1029,10 +1054,10 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
     };
 
     std::lock_guard<std::mutex> lock(ctx->mu);
-    const int t = ctx->nice_next;
-    NiceJob &job = ctx->nice[t];
-    if (job.active)
+    const int t = free_slot(ctx->nice, ctx->nice_next);
+    if (t < 0)
         return fail(NICE_ERR_INVALID, "three niceonly fields already in flight on this context; collect one first");
+    NiceJob &job = ctx->nice[t];
     job = NiceJob{};
     job.base = base;
     job.t0 = t0;
@@ -1414,7 +1439,7 @@ int nice_niceonly_collect(nice_ctx *ctx, int t, nice_number *out, size_t cap, si
                     }
 #endif
                     if (c[25])
-                        return fail(NICE_ERR_CAPACITY, "device MSD queue overflow (msd_floor too small "
+                        return fail(NICE_ERR_MSD_OVERFLOW, "device MSD queue overflow (msd_floor too small "
                                                        "for chunk_size); use msd_where = host");
                     uint64_t cand, nums;
                     std::memcpy(&cand, c + 28, 8);

@@ -282,8 +282,20 @@ def process_field_both_pipelined(ex: PipelinedExchange, range_: FieldSize, base:
     dist, group = ex.dist, ex.group
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     (hist, near), (nice, stats) = _both_shards(range_, base, ctx, rank, world, nice_opts)
-    vec = list(hist[: base + 1]) + _onehot(rank, world, len(near)) + _onehot(rank, world, len(nice))
+    vec = exchange_vector(hist, base, rank, world, len(near), len(nice))
     return finish_both(ex, ex.submit(vec, (base, near, nice, stats)))
+
+
+MAX_BINS = 129  # histogram bins of the widest base (128) -- the exchange vector's fixed head
+
+
+def exchange_vector(hist, base: int, rank: int, world: int, n_near: int, n_nice: int) -> List[int]:
+    """A field's pipelined exchange vector: the histogram zero-padded to the
+    widest base's 129 bins, then every rank's near-miss and nice counts (one-hot
+    blocks).  Its length depends only on the world size, so consecutive fields
+    of different bases share the exchange's buffers (no drain in between)."""
+    head = list(hist[: base + 1]) + [0] * (MAX_BINS - base - 1)
+    return head + _onehot(rank, world, n_near) + _onehot(rank, world, n_nice)
 
 
 def finish_both(ex: PipelinedExchange, collected):
@@ -293,9 +305,9 @@ def finish_both(ex: PipelinedExchange, collected):
     red, (base, near, nice, stats) = collected
     world = ex.dist.get_world_size(ex.group)
     hist = red[: base + 1]
-    near_rows = _gather_rows(near, ex.dist, ex.group, counts=red[base + 1: base + 1 + world])
+    near_rows = _gather_rows(near, ex.dist, ex.group, counts=red[MAX_BINS: MAX_BINS + world])
     nice_rows = sorted(_gather_rows([(n, base) for n in nice], ex.dist, ex.group,
-                                    counts=red[base + 1 + world:]))
+                                    counts=red[MAX_BINS + world:]))
     det = FieldResults(
         distribution=[UniquesDistributionSimple(i, hist[i]) for i in range(1, base + 1)],
         nice_numbers=[NiceNumberSimple(n, u) for n, u in near_rows])
@@ -371,8 +383,7 @@ class FieldPipeline:
         if self.ex is None:
             return (range_, _results(hist, near, base), FieldResults(
                 distribution=[], nice_numbers=[NiceNumberSimple(n, base) for n in nice]), stats)
-        vec = list(hist[: base + 1]) + _onehot(self.rank, self.world, len(near)) \
-            + _onehot(self.rank, self.world, len(nice))
+        vec = exchange_vector(hist, base, self.rank, self.world, len(near), len(nice))
         return self._finish(self.ex.submit(vec, (base, near, nice, stats, range_)))
 
     def _finish(self, collected):

@@ -99,6 +99,30 @@ def test_cpu_niceonly_matches_oracle(base, start, size, k):
         assert _nice(got) == [(n, u) for n, u in want.nice_numbers], (base, threads)
 
 
+@pytest.mark.parametrize("base,start,end,count", [
+    (10, 1, 47, 4),         # below b10's range: [(3,10),(8,10),(9,10),(24,10)]
+    (16, 1, 60, 5),
+    (25, 1, 10 ** 4, 19),
+    (40, 1, 10 ** 5, 265),
+    (12, 1, 200, None),
+    (64, 10 ** 6, 10 ** 6 + 5 * 10 ** 5, None),
+])
+def test_cpu_niceonly_below_range_matches_oracle(base, start, end, count):
+    # get_is_nice has no digit-count test (client_process.rs:258-290): below a
+    # base's valid range every n whose n^2 and n^3 digits are all distinct is
+    # listed by process_range_niceonly (:439-465)
+    want, _ = O.process_range_niceonly(start, end, base, 2)
+    want = [(n, u) for n, u in want.nice_numbers]
+    if count is not None:
+        assert len(want) == count
+    if base == 10:
+        assert want == [(3, 10), (8, 10), (9, 10), (24, 10)]
+    for threads in (1, 4):
+        got = N.process_range_niceonly_cpu(N.FieldSize(start, end), base, N.StrideTable.new(base, 2),
+                                           threads=threads)
+        assert _nice(got) == want, (base, threads)
+
+
 def test_cpu_errors_and_capacity():
     with pytest.raises(N.NiceError):
         N.process_range_detailed_cpu(N.FieldSize(10, 20), 129)

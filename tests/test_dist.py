@@ -172,6 +172,17 @@ def _field_worker(rank, world, port, q):
                               [(d.num_uniques, d.count) for d in det.distribution],
                               [(n.number, n.num_uniques) for n in det.nice_numbers],
                               [n.number for n in nic.nice_numbers]) for r, det, nic, _ in got]
+    # fields of different bases back to back (the client's field stream can
+    # change base): the exchange vector keeps its width, nothing drains early
+    pipe = D.FieldPipeline(_OracleCtx(), _OracleCtx(), dist, chunk_size=997)
+    mixed = [(FieldSize(47, 2_047), 10), (FieldSize(1, 3_000), 12), (FieldSize(10 ** 6, 10 ** 6 + 900), 40),
+             (FieldSize(69, 70), 10)]
+    got = [pipe.step(f, b) for f, b in mixed]
+    got = [g for g in got if g is not None] + pipe.drain()
+    res["field_pipeline_mixed"] = [((r.range_start, r.range_end), len(det.distribution),
+                                    [(d.num_uniques, d.count) for d in det.distribution],
+                                    [(n.number, n.num_uniques) for n in det.nice_numbers],
+                                    [n.number for n in nic.nice_numbers]) for r, det, nic, _ in got]
     q.put((rank, res))
     dist.destroy_process_group()
 
@@ -214,6 +225,13 @@ def test_two_rank_field_sharding_matches_single_process():
         w = O.process_range_detailed(a, b, 10)
         assert (d, near) == (w.distribution, w.nice_numbers)
         assert nice == _oracle_niceonly_shard(a, b, 10, 997)
+    mixed = out[0]["field_pipeline_mixed"]
+    assert [(r[0], r[1]) for r in mixed] == [((47, 2_047), 10), ((1, 3_000), 12),
+                                             ((10 ** 6, 10 ** 6 + 900), 40), ((69, 70), 10)]
+    for (a, b), base, d, near, nice in mixed:
+        w = O.process_range_detailed(a, b, base)
+        assert (d, near) == (w.distribution, w.nice_numbers), base
+        assert nice == _oracle_niceonly_shard(a, b, base, 997), base
     w = O.process_range_detailed(69, 70, 10)
     assert out[0]["tiny"] == (w.distribution, [(69, 10)])
     assert out[0]["tiny_both"] == (w.distribution, [(69, 10)], [69])

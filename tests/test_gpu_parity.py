@@ -327,6 +327,50 @@ def test_niceonly_multi_device_context():
     c.close()
 
 
+@pytest.mark.parametrize("where", MSD_WHERE)
+@pytest.mark.parametrize("path", ["fused", "wave"])
+def test_niceonly_below_range_windows(ctx, where, path):
+    """Windows below a base's valid range, where get_is_nice lists every n
+    whose n^2 and n^3 digits are merely distinct (no digit-count test,
+    client_process.rs:258-290; process_range_niceonly lists them, :439-465):
+    b10 [1, 47) -> 3, 8, 9, 24; b40 [1, 1e5) -> 265 numbers.  Nice list,
+    candidates and MSD ranges against the oracle on the same chunk grid, for
+    both MSD placements, through the fused per-chunk kernel (client chunking)
+    and the wave kernel (1e8 chunks)."""
+    chunk = 10 ** 8 if path == "wave" else 0
+    cases = [(10, 1, 47, 4), (16, 1, 60, 5), (25, 1, 10 ** 4, 19), (40, 1, 10 ** 5, 265),
+             (12, 1, 2_000, None), (64, 10 ** 6, 10 ** 6 + 5 * 10 ** 5, None)]
+    for base, a, b, count in cases:
+        res, cands, ranges, _ = O.process_field_niceonly_sq(a, b, base, 4, chunk)
+        want = [n for n, _ in res.nice_numbers]
+        if count is not None:
+            assert len(want) == count, base
+        lst, st = ctx.niceonly_raw(a, b, base, chunk_size=chunk, msd_where=where)
+        assert lst == want, (base, a, b)
+        assert (st.candidates, st.ranges) == (cands, ranges), (base, a, b)
+    assert ctx.niceonly_raw(1, 47, 10, chunk_size=chunk, msd_where=where)[0] == [3, 8, 9, 24]
+
+
+def test_slots_reused_after_out_of_order_collect(ctx):
+    """Tickets are collected in any order (nice_hip.h): after submit t0, t1, t2
+    and collect t1, a new submit takes the free slot instead of failing."""
+    s40 = O.base_range(40)[0]
+    fields = [(s40 + k * 10 ** 6, s40 + (k + 1) * 10 ** 6) for k in range(4)]
+    want = [ctx.detailed_raw(a, b, 40) for a, b in fields]
+    t = [ctx.detailed_submit(a, b, 40) for a, b in fields[:3]]
+    assert ctx.detailed_collect(t[1], 40) == want[1]
+    t3 = ctx.detailed_submit(*fields[3], 40)
+    assert t3 == t[1]
+    assert [ctx.detailed_collect(x, 40) for x in (t[0], t[2], t3)] == [want[0], want[2], want[3]]
+    nice_want = [ctx.niceonly_raw(a, b, 40) for a, b in fields]
+    t = [ctx.niceonly_submit(a, b, 40) for a, b in fields[:3]]
+    got2 = ctx.niceonly_collect(t[2])
+    t3 = ctx.niceonly_submit(*fields[3], 40)
+    got = [ctx.niceonly_collect(x) for x in (t[0], t[1], t3)]
+    for (l, st), (wl, wst) in zip([got[0], got[1], got2, got[2]], nice_want):
+        assert l == wl and st.candidates == wst.candidates and st.ranges == wst.ranges
+
+
 def test_residue_empty_base(ctx):
     assert ctx.niceonly_raw(100, 200, 11)[0] == []
 
