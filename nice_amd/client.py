@@ -9,10 +9,16 @@ explicit --range/--base; the reference's HTTP claim/submit/validate transport
 (client_api_*.rs) is out of scope, so --validate
 compares against a JSON file of a canonical submission instead of the server.
 
-Processing runs on the GPU path for every mode: the reference's CPU
-(rayon) path is replaced by the library, which has no CPU fallback.
+With --gpu a field runs on the HIP path (process_range_*_gpu, one call per
+field).  Without it, the reference's CPU mode (main.rs:154-207): the field is
+cut into client chunks (1e6 * clamp(ceil(size / 1e11), 1, 1000)), the chunks
+are processed by --threads workers through the library's CPU API
+(nice_cpu_process_range_detailed / _niceonly, the reference's
+process_range_detailed / process_range_niceonly), and the per-chunk results are
+merged in chunk order (compile_results).  No GPU is touched in that mode.
 
     python -m nice_amd detailed --benchmark extra-large --gpu
+    python -m nice_amd --benchmark base-ten            # CPU mode
 """
 from __future__ import annotations
 
@@ -100,6 +106,37 @@ def validate_results(submit: DataToServer, canon: dict, mode: SearchMode) -> boo
     return ok
 
 
+def process_field_sync(claim: DataToClient, mode: SearchMode, args, ctx=None):
+    """process_field_sync (client/src/main.rs:120-208): the GPU call for the
+    whole field with --gpu, else the CPU path per client chunk on --threads
+    workers (rayon par_iter in the reference), results in chunk order."""
+    field = claim.field()
+    if args.gpu:
+        if mode is SearchMode.DETAILED:
+            return [api.process_range_detailed_gpu(ctx, field, claim.base)]
+        return [api.process_range_niceonly_gpu(ctx, field, claim.base, threads=args.threads,
+                                               msd_floor=args.msd_floor)]
+    from concurrent.futures import ThreadPoolExecutor
+    from .dist import client_chunk_size
+    from .types import FieldSize
+    chunk = client_chunk_size(field.range_size)
+    chunks = [FieldSize(a, min(field.range_end, a + chunk))
+              for a in range(field.range_start, field.range_end, chunk)]
+    if mode is SearchMode.DETAILED:
+        def work(c):
+            return api.process_range_detailed_cpu(c, claim.base)
+    else:
+        # main.rs:173-180: one stride table for the field (k = 2, main.rs:19)
+        table = api.StrideTable.new(claim.base, 2)
+
+        def work(c):
+            return api.process_range_niceonly_cpu(c, claim.base, table)
+    # ctypes releases the GIL inside the library call, so the workers run the
+    # chunks in parallel on the host cores
+    with ThreadPoolExecutor(max(1, args.threads)) as pool:
+        return list(pool.map(work, chunks))
+
+
 def run_once(args, ctx) -> int:
     mode = SearchMode.DETAILED if args.mode == "detailed" else SearchMode.NICEONLY
     if args.benchmark:
@@ -114,17 +151,13 @@ def run_once(args, ctx) -> int:
                   "use --benchmark or --base/--range")
         return 2
     t0 = time.perf_counter()
-    if mode is SearchMode.DETAILED:
-        res = api.process_range_detailed_gpu(ctx, claim.field(), claim.base)
-    else:
-        res = api.process_range_niceonly_gpu(ctx, claim.field(), claim.base,
-                                             threads=args.threads, msd_floor=args.msd_floor)
+    results = process_field_sync(claim, mode, args, ctx)
     elapsed = time.perf_counter() - t0
     # The reference prints this line with --no-progress or --gpu (main.rs:358-371);
     # this client has no progress bar, so it always does.
     log.info("✓ Processed %.2e numbers in %.2fs (%.2e numbers/sec)",
              claim.range_size, elapsed, claim.range_size / elapsed)
-    submit = compile_results([res], claim, args.username, mode)
+    submit = compile_results(results, claim, args.username, mode)
     log.debug("Submit Data: %s", json.dumps(submit.to_json()))
     for n in submit.nice_numbers:
         log.info("Nice number: %d (%d uniques)", n.number, n.num_uniques)
@@ -144,12 +177,16 @@ def main(argv=None) -> int:
     level = {"off": logging.CRITICAL + 10, "error": logging.ERROR, "warn": logging.WARNING,
              "info": logging.INFO, "debug": logging.DEBUG, "trace": logging.DEBUG}[args.log_level]
     logging.basicConfig(level=level, format="%(asctime)s %(levelname)s %(message)s")
-    log.info("GPU_BATCH_SIZE = %d", api.GPU_BATCH_SIZE)
-    try:
-        ctx = api.GpuContext(_devices(args.gpu_device))
-    except api._lib.NiceError as e:
-        log.error("GPU processing error: %s", e)
-        return 1
+    ctx = None
+    if args.gpu:  # main.rs:592-625: the GPU context only in GPU mode
+        log.info("GPU_BATCH_SIZE = %d", api.GPU_BATCH_SIZE)
+        try:
+            ctx = api.GpuContext(_devices(args.gpu_device))
+        except api._lib.NiceError as e:
+            log.error("GPU processing error: %s", e)
+            return 1
+    else:
+        log.info("CPU mode: %d threads", args.threads)
     while True:
         rc = run_once(args, ctx)
         if rc or not args.repeat:

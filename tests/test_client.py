@@ -68,3 +68,46 @@ def test_client_benchmark_base_ten_validates(tmp_path, capsys):
     canon["nice_numbers"] = []
     p.write_text(json.dumps(canon))
     assert C.main(["niceonly", "--benchmark", "base-ten", "--gpu", "--validate", str(p)]) == 1
+
+
+def test_client_cpu_mode_base_ten(tmp_path, capsys):
+    """Without --gpu the client runs the reference's CPU mode (main.rs:154-207):
+    base-ten lists (69, 10) with the process_detailed_b10 distribution, no
+    GPU touched (this runs in the CPU suite)."""
+    from oracle import oracle as O
+    want = O.process_range_detailed(47, 100, 10)
+    canon = {"nice_numbers": [{"number": str(n), "num_uniques": u} for n, u in want.nice_numbers],
+             "unique_distribution": [{"num_uniques": u, "count": c} for u, c in want.distribution]}
+    assert want.nice_numbers == [(69, 10)]
+    p = tmp_path / "canon.json"
+    p.write_text(json.dumps(canon))
+    assert C.main(["--benchmark", "base-ten", "--validate", str(p)]) == 0
+    assert "Validation passed" in capsys.readouterr().out
+    assert C.main(["niceonly", "--benchmark", "base-ten", "--validate", str(p)]) == 0
+    canon["nice_numbers"] = []
+    p.write_text(json.dumps(canon))
+    assert C.main(["niceonly", "--benchmark", "base-ten", "--validate", str(p)]) == 1
+
+
+def test_client_cpu_mode_chunks_merge_like_one_range():
+    """CPU mode cuts the field into client chunks and merges them in order:
+    a 2.5e6 b40 field (three 1e6 chunks, the last ragged) on 3 workers equals
+    the oracle over the whole range; niceonly below b40's range lists the
+    265 numbers of [1, 1e5) (get_is_nice has no digit-count test)."""
+    from oracle import oracle as O
+    s = O.base_range(40)[0]
+    claim = DataToClient(0, 40, s, s + 2_500_000, 2_500_000)
+    args = C.parse_args(["--threads", "3"])
+    res = C.process_field_sync(claim, SearchMode.DETAILED, args)
+    assert len(res) == 3
+    sub = C.compile_results(res, claim, "u", SearchMode.DETAILED)
+    want = O.process_range_detailed(s, s + 2_500_000, 40)
+    assert [(d.num_uniques, d.count) for d in sub.unique_distribution if d.count] == \
+        [x for x in want.distribution if x[1]]
+    assert [(n.number, n.num_uniques) for n in sub.nice_numbers] == want.nice_numbers
+    claim = DataToClient(0, 40, 1, 10 ** 5, 10 ** 5 - 1)
+    res = C.process_field_sync(claim, SearchMode.NICEONLY, args)
+    sub = C.compile_results(res, claim, "u", SearchMode.NICEONLY)
+    want, _ = O.process_range_niceonly(1, 10 ** 5, 40)
+    assert [(n.number, n.num_uniques) for n in sub.nice_numbers] == want.nice_numbers
+    assert len(want.nice_numbers) == 265
