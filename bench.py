@@ -40,15 +40,13 @@ import os
 import sys
 import time
 
-# Hardware queues per process (HIP's default is 4): torch's stream, RCCL's
-# stream and the two mode streams must not share a queue, or the niceonly
-# pass serialises behind the detailed kernel (torchrun 1 rank, r01: 2.86 ms
-# per step with 4 queues, 2.61 with 8).  Set before HIP initialises; an
-# exported value below 8 (the box exports HIP's default, 4) is raised, and the
-# value used is recorded in the JSON line's config.
+# Hardware queues per process: HIP's default (4, what the GPU box exports and
+# what a Rust client linking libnice_hip.so gets) unless --hw-queues N asks for
+# another value (A/B runs).  Set before HIP initialises; the value used and the
+# exported one are recorded in the JSON line's config.
 HW_QUEUES_EXPORTED = os.environ.get("GPU_MAX_HW_QUEUES")
-if int(HW_QUEUES_EXPORTED or 0) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+if "--hw-queues" in sys.argv:
+    os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[sys.argv.index("--hw-queues") + 1]
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -84,6 +82,8 @@ def parse():
                    help="A/B experiments: load the probe build (env tuning knobs live only there)")
     p.add_argument("--two-ctx", action="store_true",
                    help="A/B: detailed and niceonly on separate contexts")
+    p.add_argument("--hw-queues", type=int, default=None,
+                   help="GPU_MAX_HW_QUEUES for this process (default: as exported, HIP default 4)")
     p.add_argument("--sync", action="store_true",
                    help="synchronous library calls (no cross-field pipelining)")
     return p.parse_args()
@@ -93,9 +93,13 @@ TRAFFIC_FILES = ("profiles/r02/traffic.json", "profiles/r01/traffic.json")
 
 
 def pmc_traffic():
-    """HBM bytes per launch of the detailed kernel on the 1e9 b40 field, from
-    the newest committed PMC pass (scripts/gpu_pmc.sh -> scripts/traffic_json.py,
-    FETCH_SIZE x2 + WRITE_SIZE); (bytes, file) or (None, None)."""
+    """HBM bytes per launch of the detailed kernel on the 1e9 b40 field: from
+    the PMC passes of this bench command (profiles/r03/pmc_bench.json,
+    FETCH_SIZE x2 + WRITE_SIZE), else the older detailed-only passes
+    (scripts/traffic_json.py); (bytes, file) or (None, None)."""
+    hw = pmc_bench()
+    if hw is not None and "traffic_bytes" in hw[0]:
+        return hw[0]["traffic_bytes"], hw[1]
     for rel in TRAFFIC_FILES:
         try:
             with open(os.path.join(ROOT, rel)) as f:
@@ -103,6 +107,22 @@ def pmc_traffic():
         except (OSError, KeyError, ValueError):
             continue
     return None, None
+
+
+PMC_BENCH_FILES = ("profiles/r03/pmc_bench.json",)
+
+
+def pmc_bench():
+    """Counter-derived figures of the fd2 kernel from the committed rocprofv3
+    --pmc passes of this bench command (scripts/pmc_bench.py); (derived, file)
+    or None."""
+    for rel in PMC_BENCH_FILES:
+        try:
+            with open(os.path.join(ROOT, rel)) as f:
+                return json.load(f)["derived"], rel
+        except (OSError, KeyError, ValueError):
+            continue
+    return None
 
 
 def rank_field(base_start: int, rank: int, size: int = FIELD_SIZE):
@@ -179,7 +199,7 @@ def cpu_baseline(start, target_s, base=BASE, field=FIELD_SIZE):
     rate extrapolated to the field), the niceonly leg on the whole field."""
     from oracle import oracle as O
     th, how = cpu_share()
-    probe = 4_000_000
+    probe = 20_000_000  # long enough that thread start-up does not skew the rate
     t = time.perf_counter()
     O.process_field_detailed_mt(start, start + probe, base, th)
     rate = probe / (time.perf_counter() - t)
@@ -193,7 +213,7 @@ def cpu_baseline(start, target_s, base=BASE, field=FIELD_SIZE):
     O.process_field_niceonly_mt(start, start + field, base, th)
     tn = time.perf_counter() - t
     nice_rate = field / tn
-    combined = 2 * field / (field / det_rate + tn)
+    combined = field / (field / det_rate + tn)  # one field, both modes (as `value`)
     # the reference client's default thread count (--threads 4,
     # client/src/main.rs:94), on a smaller detailed sample
     n4 = max(1_000_000, int(det_rate / th * 4 * target_s / 3) // 1_000_000 * 1_000_000)
@@ -206,7 +226,7 @@ def cpu_baseline(start, target_s, base=BASE, field=FIELD_SIZE):
     return {"value": combined, "unit": "numbers/s", "cores": th, "kind": "port",
             "nproc": th, "cores_source": how, "host_logical_cpus": os.cpu_count(),
             "cpu_model": cpu_model(),
-            "threads4": {"value": 2 * field / (field / det4 + tn4), "cores": 4,
+            "threads4": {"value": field / (field / det4 + tn4), "cores": 4,
                          "detailed_numbers_per_sec": det4, "niceonly_numbers_per_sec": field / tn4,
                          "sample": f"detailed: first {n4:.3g} n; niceonly: whole field"},
             "sample": f"detailed: first {n:.3g} n of the field on {th} threads ({td:.1f} s, "
@@ -317,13 +337,39 @@ def main():
     kernel_ms.clear()
 
     elapsed = timed(step, args.steps, barrier_sync, dist, tail=tail)
+    # Event spans of the detailed launches inside the timed region: consecutive
+    # fields run on different slots' streams and overlap at their edges by
+    # design (a field's first workgroups fill the CUs the previous field's last
+    # ones leave idle), so a span holds its neighbours' work too; reported as
+    # pipelined_launch_span_ms, not used as a launch duration.
     pipelined_kms = sum(kernel_ms) / len(kernel_ms) if kernel_ms else None
 
-    # Roofline phase: in the pipeline consecutive fields' kernels overlap on
-    # two streams (that is the point), so a launch's event span includes its
-    # neighbours'.  The dominant kernel's duration is measured here on its
-    # own: this rank's detailed shard, launched back to back with the host
-    # waiting in between (no overlap), HIP events on the launch stream.
+    # Each mode alone over the same field, same pipeline, same timing rules
+    # (BOTH modes check every n of the field; these are the per-mode rates).
+    per_mode = {}
+    if args.mode == "both" and not args.sync:
+        for name, sel in (("detailed", (True, False)), ("niceonly", (False, True))):
+            p1 = D.FieldPipeline(det_ctx if sel[0] else _Skip(), nice_ctx if sel[1] else _Skip(),
+                                 dist, depth=args.depth, **nice_opts)
+
+            def step1(p1=p1):
+                r = p1.step(field, base)
+                if r is not None and sel[0]:
+                    assert sum(d.count for d in r[1].distribution) == job_size
+
+            def tail1(p1=p1):
+                for r in p1.drain():
+                    if sel[0]:
+                        assert sum(d.count for d in r[1].distribution) == job_size
+            for _ in range(args.warmup):
+                step1()
+            tail1()
+            per_mode[name] = timed(step1, args.steps, barrier_sync, dist, tail=tail1)
+
+    # The dominant kernel's launch duration: this rank's detailed shard
+    # launched back to back with the host waiting in between (no overlap), HIP
+    # events on the launch stream; the same dispatches are the last fd2 ones in
+    # a rocprofv3 kernel trace of this command (scripts/trace_summary.py).
     iso_ms = []
     if modes[0]:
         s_r, e_r = D.shard_bounds(field.range_start, field.range_end, rank, world)
@@ -354,8 +400,9 @@ def main():
                        None, tail=solo_tail) / args.steps
         dist.barrier()
 
-    nmodes = int(modes[0]) + int(modes[1])
-    value = nmodes * job_size * args.steps / elapsed
+    # the metric: field numbers / elapsed, one field per step --
+    # every n of it checked in both modes (detailed AND niceonly)
+    value = job_size * args.steps / elapsed
     if rank != 0:
         if args.sync:
             runner.close()
@@ -372,6 +419,8 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
+        "value_definition": "field numbers x steps / elapsed; one step = ONE field, every n checked in "
+                            "both modes (detailed AND niceonly), as BASELINE.md defines the metric",
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
@@ -394,10 +443,13 @@ def main():
             "pipelined": not args.sync,
             "pipeline_depth": None if args.sync else args.depth,
             "probe_lib": PROBE_LIB,
-            "gpu_max_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
+            "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
             "gpu_max_hw_queues_exported": HW_QUEUES_EXPORTED,
         },
     }
+    for name, el in per_mode.items():
+        line[f"{name}_numbers_per_sec"] = job_size * args.steps / el
+        line[f"{name}_ms_per_step"] = el / args.steps * 1e3
     if t1 is not None:
         line["t1_ms_per_step"] = t1 * 1e3
         line["strong_efficiency"] = t1 / (world * elapsed / args.steps)
@@ -413,16 +465,36 @@ def main():
             "traffic_source": pmc_traffic()[1] if default_cfg and world == 1 else None,
             "kernel_ms": kms, "numbers_per_launch": shard,
             "work_per_unit": f"{w_alg} int32 ops per n (4 per digit x {base} digits, SURVEY 8d)",
-            "pipelined_frac": step_rate / PEAK_INT32_TOPS,
+            "step_frac": step_rate / PEAK_INT32_TOPS,
             "pipelined_launch_span_ms": pipelined_kms,
-            "note": "integer-VALU/LDS bound (no HBM stream, no contraction); kernel_ms = median "
-                    "duration of this rank's detailed shard (main + tail launch) from HIP events "
-                    "on the launch stream, launched back to back without overlap after the timed "
-                    "region; pipelined_frac = the same work per timed step (both modes share "
-                    "the GPU, consecutive fields overlap on two streams); traffic: HBM bytes per "
-                    "launch from the committed PMC pass (traffic_source, FETCH_SIZE x2 + "
-                    "WRITE_SIZE), the field's bounds are the only input",
+            "note": "integer-VALU/LDS bound (no HBM stream, no contraction). kernel_ms = median "
+                    "duration of this rank's detailed shard launched alone (HIP events on its "
+                    "launch stream, after the timed region; the same dispatches close the rocprofv3 "
+                    "trace of this command). step_frac = the same work per timed step, both modes "
+                    "and the pipeline's overlap of consecutive fields included (it can pass 1: the "
+                    "SURVEY 8d charge of 4 int32 ops per digit is a model of a division-per-digit "
+                    "kernel, and this one does the digit work in fewer instructions, partly as LDS "
+                    "table lookups). frac_hw / hw: what the hardware counters of this command show "
+                    "(committed rocprofv3 --pmc passes). traffic: HBM bytes per launch "
+                    "(traffic_source, FETCH_SIZE x2 + WRITE_SIZE); the field's bounds are the only "
+                    "input",
         }
+        hw = pmc_bench() if default_cfg and world == 1 else None
+        if hw is not None:
+            der, src = hw
+            line["roofline"]["frac_hw"] = der.get("valu_busy")
+            line["roofline"]["hw"] = {
+                "source": src, "valu_busy": der.get("valu_busy"),
+                "valu_lane_ops_per_n": der.get("valu_lane_ops_per_n"),
+                "valu_issue_frac": der["valu_lane_ops_per_n"] * shard / (kms / 1e3) / 1e12
+                / PEAK_INT32_TOPS if "valu_lane_ops_per_n" in der else None,
+                "lds_instr_per_n": der.get("lds_instr_per_n"),
+                "lds_conflict_frac": der.get("lds_conflict_frac"),
+                "note": "frac_hw = VALUBusy of the fd2 kernel (rocprofv3 --pmc passes of this "
+                        "bench command); valu_issue_frac = executed VALU lane-ops (SQ_INSTS_VALU x "
+                        "64) per second of kernel_ms over the 32-lanes/clk peak: the SIMDs issue "
+                        "many int ops at half rate (profiles/r01/isa_issue_rates_gfx950.log) and "
+                        "the LDS lookups replace most of the per-digit VALU work"}
     st = last_stats[0]
     if st is not None:
         line["niceonly"] = {"ranges": st.ranges, "range_numbers": st.range_numbers,

@@ -5,25 +5,8 @@
 // for every n in a segment, count the distinct base-b digits of n^2 and n^3,
 // histogram the counts and list the near-misses (count > cutoff).
 //
-// This file: the generic kernel.  The finite-difference kernel for in-range
-// segments is in fd_detailed.hip.  Summary of that design:
-//
-// detailed_fd_kernel<BASE, Variant>  (segments inside the base's valid range)
-//   Each thread walks a contiguous run of n and never multiplies: n^2 and n^3
-//   are kept directly in radix B = BASE^2 limbs and advanced by finite
-//   differences,
-//       S = n^2   += D1,  D1 = 2n+1        += 2
-//       C = n^3   += E1,  E1 = 3n^2+3n+1   += E2,  E2 = 6n+6 += 6
-//   so no digit is ever divided out: every limb IS two base-b digits, and its
-//   digit mask comes from one LDS table lookup (B entries).  Limb additions
-//   use the 32-bit carry chain (v_add_co/v_addc_co): one operand is stored
-//   biased by 2^32 - B so the hardware carry-out is exactly the radix-B carry.
-//   Only the low limbs change every step; the high limbs of S and C change on
-//   a carry out of the low part (probability ~D1/B^SL per step), so their
-//   masks are cached in registers and recomputed on that rare branch.
-//   Histograms are per-thread LDS counters ([bin][thread], conflict-free),
-//   reduced per workgroup with wave shuffles and flushed with one global
-//   atomic per bin per workgroup.
+// This file: the generic kernel.  Segments inside a base's valid range run
+// the finite-difference kernel instead (fd2_kernel.hpp).
 //
 // detailed_generic_kernel  (any base 2..128, any n < 2^128)
 //   Per-n multiply + chunked radix extraction with a runtime base.  Used for

@@ -41,11 +41,6 @@ struct DetailedLaunch {
     FieldFinish fin;             // fd2 only; see FieldFinish
 };
 
-// Bases with a finite-difference kernel (valid only for n inside the base's
-// range, where n^2 and n^3 have fixed digit counts).
-bool fd_supported(uint32_t base);
-// Launch the FD kernel over an in-range segment.  grid_cap: max workgroups.
-hipError_t launch_detailed_fd(const DetailedLaunch &p, int num_cus, hipStream_t s, int variant = 0);
 // Production FD kernel (fd2_detailed.hip): bases 40, 50, 80, in-range segments.
 bool fd2_supported(uint32_t base);
 hipError_t launch_detailed_fd2(const DetailedLaunch &p, int num_cus, hipStream_t s);

@@ -74,6 +74,18 @@ inline int no_time() {
 #endif
 }
 
+// Streams of a device's slots: bit 0 = the slots share ONE detailed stream
+// (consecutive detailed fields run back to back instead of overlapping at
+// their edges), bit 1 = they share one niceonly stream.
+inline int shared_streams() {
+#ifdef NICE_PROBES
+    static const int v = getenv("NICE_SHARED_STREAMS") ? atoi(getenv("NICE_SHARED_STREAMS")) : 0;
+    return v;
+#else
+    return 0;
+#endif
+}
+
 inline int slots_used() {
 #ifdef NICE_PROBES
     static const int n = getenv("NICE_SLOTS") ? std::max(1, std::min(kSlots, atoi(getenv("NICE_SLOTS")))) : kSlots;
@@ -138,6 +150,7 @@ struct ListBuf {
 // field i's last ones leave idle), state block, results and MSD buffers.
 struct Slot {
     hipStream_t stream = nullptr;   // detailed
+    bool own_stream = false, own_nstream = false;  // false: shared with slot 0 (shared_streams)
     hipStream_t nstream = nullptr;  // niceonly: high priority, so its chain of short,
                                     // dependent MSD launches is not queued behind the
                                     // detailed kernels' workgroups
@@ -301,14 +314,24 @@ int ensure_msd(Slot &sl, uint32_t q_cap, uint32_t leaf_cap, uint64_t scratch_nod
     return NICE_OK;
 }
 
-int slot_init(Device &d, Slot &sl) {
-    HIPCHK(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+int slot_init(Device &d, Slot &sl, const Slot *share) {
+    if (share && (shared_streams() & 1)) {
+        sl.stream = share->stream;
+    } else {
+        HIPCHK(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+        sl.own_stream = true;
+    }
     int least = 0, greatest = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
 #ifdef NICE_PROBES
     if (getenv("NICE_NICE_PRIO") && atoi(getenv("NICE_NICE_PRIO")) == 0) greatest = least;
 #endif
-    HIPCHK(hipStreamCreateWithPriority(&sl.nstream, hipStreamNonBlocking, greatest));
+    if (share && (shared_streams() & 2)) {
+        sl.nstream = share->nstream;
+    } else {
+        HIPCHK(hipStreamCreateWithPriority(&sl.nstream, hipStreamNonBlocking, greatest));
+        sl.own_nstream = true;
+    }
     HIPCHK(hipMalloc(&sl.d_nice_count, 4));
     // hist bins and list counters in one block: one memset per field at most.
     HIPCHK(hipMalloc(&sl.d_state, kStateBytes));
@@ -338,8 +361,8 @@ int device_init(Device &d, int id) {
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, id));
     d.num_cus = prop.multiProcessorCount;
-    for (auto &sl : d.slot) {
-        int rc = slot_init(d, sl);
+    for (int i = 0; i < kSlots; i++) {
+        int rc = slot_init(d, d.slot[i], i ? &d.slot[0] : nullptr);
         if (rc) return rc;
     }
     return NICE_OK;
@@ -368,8 +391,8 @@ void device_free(Device &d) {
         if (sl.msd.leaves) (void)hipFree(sl.msd.leaves);
         if (sl.msd.counters) (void)hipFree(sl.msd.counters);
         if (sl.msd.scratch) (void)hipFree(sl.msd.scratch);
-        if (sl.stream) (void)hipStreamDestroy(sl.stream);
-        if (sl.nstream) (void)hipStreamDestroy(sl.nstream);
+        if (sl.stream && sl.own_stream) (void)hipStreamDestroy(sl.stream);
+        if (sl.nstream && sl.own_nstream) (void)hipStreamDestroy(sl.nstream);
         if (sl.d_nice_count) (void)hipFree(sl.d_nice_count);
         if (sl.d_nice_done) (void)hipFree(sl.d_nice_done);
         if (sl.d_state) (void)hipFree(sl.d_state);
@@ -439,14 +462,6 @@ int validate_detailed(uint32_t base, u128 size, const uint64_t *hist, size_t n, 
     return NICE_OK;
 }
 
-#ifdef NICE_PROBES
-// FD kernel variant (0 = production choice; others for scripts/fd_sweep.py).
-int fd_variant() {
-    const char *v = getenv("NICE_FD_VARIANT");
-    return v ? atoi(v) : 0;
-}
-#endif
-
 // Enqueue the detailed kernels for [s, e) on one device (async).
 // Enqueue the detailed kernels for [s, e) on one device (async): generic
 // kernel outside the base's valid range, FD kernel inside.  Returns in
@@ -475,17 +490,9 @@ int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *f
 #ifdef NICE_PROBES
             if (getenv("NICE_FD2_NOFIN")) p.fin = nice::FieldFinish{nullptr, nullptr, 0};  // probe: finish kernel
 #endif
-#ifdef NICE_PROBES
-            const int var = fd_variant();
-            const bool fd2 = fd && var == 0 && nice::fd2_supported(base);
-            hipError_t err = !fd ? nice::launch_detailed_generic(p, d.num_cus, sl.stream)
-                             : fd2 ? nice::launch_detailed_fd2(p, d.num_cus, sl.stream)
-                                   : nice::launch_detailed_fd(p, d.num_cus, sl.stream, var);
-#else
             const bool fd2 = fd;
             hipError_t err = fd ? nice::launch_detailed_fd2(p, d.num_cus, sl.stream)
                                 : nice::launch_detailed_generic(p, d.num_cus, sl.stream);
-#endif
             if (err != hipSuccess)
                 return fail(NICE_ERR_HIP, std::string("detailed launch: ") + hipGetErrorString(err));
             if (last) *finished = fd2 && p.fin.out_mapped;
@@ -495,11 +502,7 @@ int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *f
         return NICE_OK;
     };
     u128 rs = 0, re = 0;
-#ifdef NICE_PROBES
-    const bool fd_base = nice::fd2_supported(base) || (fd_variant() && nice::fd_supported(base));
-#else
     const bool fd_base = nice::fd2_supported(base);
-#endif
     const bool fd = fd_base && nice::base_range_cached(base, rs, re) == 1;
     if (!fd) return launch(s, e, false);
     int rc;

@@ -1,0 +1,69 @@
+"""Counter summary of the bench's dominant kernel from rocprofv3 --pmc passes of
+the bench command itself (scripts/gpu.sh pmc TAG "COUNTERS" [bench args], one
+counter group per pass), for bench.py's roofline.frac_hw:
+
+    python scripts/pmc_bench.py --numbers 1e9 --out profiles/r03/pmc_bench.json \
+        gpurun_out/pmc_bench_valu gpurun_out/pmc_bench_lds gpurun_out/pmc_bench_busy
+
+Per-dispatch means over every fd2_kernel dispatch of every pass (warmup, timed
+region and the isolated launches alike: the kernel is the same launch each
+time).  Derived:
+  valu_busy           VALUBusy / 100 (SQ_ACTIVE_INST_VALU over GRBM_GUI_ACTIVE x CUs)
+  valu_lane_ops_per_n SQ_INSTS_VALU x 64 / numbers per dispatch
+  lds_instr_per_n     SQ_INSTS_LDS x 64 / numbers
+  lds_conflict_frac   SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
+  traffic_bytes       HBM bytes: FETCH_SIZE x 2 + WRITE_SIZE (KB -> B), separate passes
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+KERNEL = "fd2_kernel"
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--numbers", type=float, required=True, help="numbers per fd2 dispatch")
+ap.add_argument("--kernel", default=KERNEL)
+ap.add_argument("--out", required=True)
+ap.add_argument("dirs", nargs="+")
+a = ap.parse_args()
+
+vals = collections.defaultdict(list)
+names = set()
+files = []
+for d in a.dirs:
+    for path in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
+        files.append(path)
+        per = collections.defaultdict(float)
+        for r in csv.DictReader(open(path)):
+            if a.kernel in r["Kernel_Name"]:
+                per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+                names.add(r["Kernel_Name"])
+        for (_, c), v in per.items():
+            vals[c].append(v)
+if not vals:
+    raise SystemExit(f"no {a.kernel} rows under {a.dirs}")
+mean = {c: sum(v) / len(v) for c, v in vals.items()}
+out = {"kernel": sorted(names), "numbers_per_dispatch": a.numbers,
+       "dispatches": {c: len(v) for c, v in vals.items()},
+       "per_dispatch": {c: round(v, 4) for c, v in sorted(mean.items())},
+       "files": [os.path.relpath(f) for f in files]}
+der = {}
+if "VALUBusy" in mean:
+    der["valu_busy"] = mean["VALUBusy"] / 100
+if "SQ_INSTS_VALU" in mean:
+    der["valu_lane_ops_per_n"] = mean["SQ_INSTS_VALU"] * 64 / a.numbers
+if "SQ_INSTS_LDS" in mean:
+    der["lds_instr_per_n"] = mean["SQ_INSTS_LDS"] * 64 / a.numbers
+if "SQ_LDS_BANK_CONFLICT" in mean and mean.get("SQ_LDS_IDX_ACTIVE"):
+    der["lds_conflict_frac"] = mean["SQ_LDS_BANK_CONFLICT"] / mean["SQ_LDS_IDX_ACTIVE"]
+if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+    # HBM bytes per dispatch: FETCH_SIZE doubled (gfx950 tallies 128-B requests
+    # at 64 B, MI355X_MICROARCH.md), WRITE_SIZE as read; both in KB
+    der["traffic_bytes"] = int(round((2 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024))
+out["derived"] = der
+with open(a.out, "w") as f:
+    json.dump(out, f, indent=1)
+print(json.dumps(der))

@@ -1,9 +1,8 @@
 """Point nice_amd at the probe build of the library (libnice_hip_probe.so,
 `make -C nice_amd probe`): the same sources compiled with -DNICE_PROBES, which
 adds the bottleneck probes (NICE_FD2_PROBE, NICE_MSD_PROBE: kernels whose
-results are wrong by design), the first-generation FD kernel
-(NICE_FD_VARIANT) and the launch tuning knobs (NICE_FD2_TCHUNK,
-NICE_FD2_MINCHUNK, NICE_FD2_WG512).  The product library ignores all of
+results are wrong by design) and the launch tuning knobs (NICE_FD2_TCHUNK,
+NICE_FD2_MINCHUNK, NICE_FD2_WG512, NICE_SLOTS, NICE_SHARED_STREAMS, ...).  The product library ignores all of
 them.  Import this module before the first nice_amd call:
 
     import probe_lib  # noqa: F401  (scripts/ on sys.path)
