@@ -66,7 +66,7 @@ def parse():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=12.0,
+    p.add_argument("--cpu-seconds", type=float, default=15.0,
                    help="target CPU work for the bounded cpu_baseline sample")
     p.add_argument("--mode", choices=["both", "detailed", "niceonly"], default="both")
     p.add_argument("--scaling", choices=["strong", "weak"], default="strong",
@@ -82,6 +82,8 @@ def parse():
                    help="A/B experiments: load the probe build (env tuning knobs live only there)")
     p.add_argument("--two-ctx", action="store_true",
                    help="A/B: detailed and niceonly on separate contexts")
+    p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                   help="N > 1: RCCL over xGMI (nccl, default) or gloo on host tensors (tests)")
     p.add_argument("--hw-queues", type=int, default=None,
                    help="GPU_MAX_HW_QUEUES for this process (default: as exported, HIP default 4)")
     p.add_argument("--sync", action="store_true",
@@ -253,8 +255,14 @@ def main():
     if "WORLD_SIZE" in os.environ:
         import torch
         import torch.distributed as dist
+        # one GPU per rank; more ranks than GPUs (the 2-rank gloo test on a
+        # one-GPU box) share devices round-robin
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     import nice_amd as N
     from nice_amd import dist as D
@@ -273,18 +281,26 @@ def main():
     modes = {"both": (True, True), "detailed": (True, False), "niceonly": (False, True)}[args.mode]
 
     def barrier_sync():
+        # the library's streams (torch is not initialised on the device at N = 1:
+        # the process's HIP runtime belongs to libnice_hip.so there)
+        det_ctx.synchronize()
+        if nice_ctx is not det_ctx:
+            nice_ctx.synchronize()
         if dist is not None:
             import torch
             torch.cuda.synchronize()
             dist.barrier()
             torch.cuda.synchronize()
+            det_ctx.synchronize()
 
     last_stats = [None]
+    checked = [0]  # fields whose whole-field results came back and were checked
 
     def check(res):
         _, det, _, st = res
         if modes[0]:
             assert sum(d.count for d in det.distribution) == job_size
+        checked[0] += 1
         last_stats[0] = st or last_stats[0]
 
     def make_pipeline(d):
@@ -336,7 +352,9 @@ def main():
     tail()
     kernel_ms.clear()
 
+    checked[0] = 0
     elapsed = timed(step, args.steps, barrier_sync, dist, tail=tail)
+    fields_checked = checked[0]  # every field of the timed region came back whole and was checked
     # Event spans of the detailed launches inside the timed region: consecutive
     # fields run on different slots' streams and overlap at their edges by
     # design (a field's first workgroups fill the CUs the previous field's last
@@ -396,8 +414,7 @@ def main():
             for _ in range(args.warmup):
                 solo_step()
             solo_tail()
-            t1 = timed(solo_step, args.steps, lambda: __import__("torch").cuda.synchronize(),
-                       None, tail=solo_tail) / args.steps
+            t1 = timed(solo_step, args.steps, det_ctx.synchronize, None, tail=solo_tail) / args.steps
         dist.barrier()
 
     # the metric: field numbers / elapsed, one field per step --
@@ -440,6 +457,7 @@ def main():
             "niceonly_msd_where": args.msd_where,
             "niceonly_chunking": "reference client (1e6 * clamp(ceil(size/1e11),1,1000))",
             "parallelism": f"{'strong' if strong else 'weak'}{world}",
+            "dist_backend": args.dist_backend if dist is not None else None,
             "pipelined": not args.sync,
             "pipeline_depth": None if args.sync else args.depth,
             "probe_lib": PROBE_LIB,
@@ -447,6 +465,7 @@ def main():
             "gpu_max_hw_queues_exported": HW_QUEUES_EXPORTED,
         },
     }
+    line["fields_checked"] = fields_checked
     for name, el in per_mode.items():
         line[f"{name}_numbers_per_sec"] = job_size * args.steps / el
         line[f"{name}_ms_per_step"] = el / args.steps * 1e3

@@ -53,6 +53,11 @@ typedef struct nice_ctx nice_ctx;
  * No JIT happens here or later: kernels are AOT-built for gfx950. */
 int nice_ctx_create(const int *devices, int n_devices, nice_ctx **out);
 void nice_ctx_destroy(nice_ctx *ctx);
+/* Wait until every stream of the context is idle (the fields in flight have
+ * finished on the device; their results still wait for *_collect).  The
+ * reference's one-stream context synchronises inside each call
+ * (client_process_gpu.rs:858-866); callers timing a pipeline bracket it with this. */
+int nice_ctx_synchronize(nice_ctx *ctx);
 int nice_device_count(int *out);
 const char *nice_last_error(void);
 

@@ -22,7 +22,7 @@ NICE_ERR_MSD_OVERFLOW = 5
 
 # Every symbol include/nice_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = (
-    "nice_ctx_create", "nice_ctx_destroy", "nice_device_count", "nice_last_error",
+    "nice_ctx_create", "nice_ctx_destroy", "nice_ctx_synchronize", "nice_device_count", "nice_last_error",
     "nice_process_range_detailed", "nice_process_range_niceonly",
     "nice_process_range_niceonly_ex", "nice_last_kernel_stats", "nice_base_range",
     "nice_near_miss_cutoff", "nice_gpu_batch_size", "nice_processing_chunk_size",
@@ -98,6 +98,7 @@ def lib():
     sig = {
         "nice_ctx_create": ([ctypes.POINTER(ctypes.c_int), i32, ctypes.POINTER(vp)], i32),
         "nice_ctx_destroy": ([vp], None),
+        "nice_ctx_synchronize": ([vp], i32),
         "nice_device_count": ([ctypes.POINTER(ctypes.c_int)], i32),
         "nice_last_error": ([], ctypes.c_char_p),
         "nice_process_range_detailed": ([vp, u64, u64, u64, u64, u32, P64, PN, sz, PSZ], i32),

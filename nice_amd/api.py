@@ -148,6 +148,10 @@ class GpuContext:
             lib().nice_ctx_destroy(self._h)
             self._h = None
 
+    def synchronize(self):
+        """Wait until every stream of this context is idle (nice_ctx_synchronize)."""
+        check(lib().nice_ctx_synchronize(self._h))
+
     def __del__(self):
         try:
             self.close()

@@ -764,6 +764,20 @@ int nice_ctx_create(const int *devices, int n_devices, nice_ctx **out) {
     return NICE_OK;
 }
 
+int nice_ctx_synchronize(nice_ctx *ctx) {
+    if (!ctx) return fail(NICE_ERR_INVALID, "null ctx");
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    for (auto &d : ctx->devs) {
+        HIPCHK(hipSetDevice(d.id));
+        for (auto &sl : d.slot) {
+            HIPCHK(hipStreamSynchronize(sl.stream));
+            HIPCHK(hipStreamSynchronize(sl.nstream));
+        }
+        if (d.aux) HIPCHK(hipStreamSynchronize(d.aux));
+    }
+    return NICE_OK;
+}
+
 void nice_ctx_destroy(nice_ctx *ctx) {
     if (!ctx) return;
     for (auto &d : ctx->devs) device_free(d);

@@ -85,3 +85,30 @@ def test_two_rank_strong_pipeline_on_gpu():
     r_ = res[0]["massive"][1] + res[1]["massive"][1]
     assert (c, r_) == (sum(w["candidates"] for w in m["windows"]), sum(w["ranges"] for w in m["windows"]))
     assert res[0]["massive"][2] == [] and res[1]["massive"][2] == []
+
+
+def test_bench_two_ranks_strong_scaling_branch():
+    """bench.py's N > 1 path end to end, as the driver's scaling run launches it
+    (torch.distributed.run, one process per rank), with gloo collectives so two
+    ranks can share the one GPU of the test box: the line carries the
+    strong-scaling fields (t1_ms_per_step, strong_efficiency, parallelism
+    strong2) and every field of the timed region came back whole and was
+    checked (fields_checked == steps)."""
+    import subprocess
+    import sys
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "6", "--warmup", "2", "--no-cpu-baseline", "--dist-backend", "gloo"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT,
+                         env=dict(os.environ, OMP_NUM_THREADS="4"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 prints the one line
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "strong2"
+    assert line["config"]["dist_backend"] == "gloo"
+    assert line["fields_checked"] == 6
+    assert line["t1_ms_per_step"] > 0 and 0 < line["strong_efficiency"] < 2
+    assert line["value"] > 0 and line["roofline"]["numbers_per_launch"] == 5 * 10 ** 8
+    assert line["detailed_numbers_per_sec"] > 0 and line["niceonly_numbers_per_sec"] > 0
