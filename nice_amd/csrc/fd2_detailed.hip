@@ -12,6 +12,10 @@
 namespace nice {
 namespace fd2 {
 
+#ifdef NICE_PROBES
+u64 *g_stamps = nullptr;  // device buffer of the phase stamps (probe build)
+#endif
+
 // ---------------------------------------------------------------------------
 // Host: limb counts per segment.  For a segment [a, e) the last FD state a
 // lane builds is for n = e (one step past its last number), so D1(e) = 2e+1,
@@ -203,3 +207,24 @@ hipError_t launch_detailed_fd2(const DetailedLaunch &p, int num_cus, hipStream_t
 }
 
 }  // namespace nice
+
+#ifdef NICE_PROBES
+// Probe build only: enable (1) the fd2 kernel's per-workgroup phase stamps
+// (kStampGroups x 16 words, zeroed), or read them into out[cap] and disable
+// (0).  Synchronous; for scripts/fd2_stamps.py.
+extern "C" int nice_probe_fd2_stamps(int enable, uint64_t *out, size_t cap) {
+    using nice::fd2::g_stamps;
+    const size_t words = (size_t)nice::fd2::kStampGroups * 16;
+    if (enable) {
+        if (!g_stamps && hipMalloc(&g_stamps, words * 8) != hipSuccess) return 2;
+        return hipMemset(g_stamps, 0, words * 8) == hipSuccess ? 0 : 2;
+    }
+    if (!g_stamps) return 1;
+    if (hipDeviceSynchronize() != hipSuccess) return 2;
+    const size_t n = cap < words ? cap : words;
+    if (out && n && hipMemcpy(out, g_stamps, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return 2;
+    (void)hipFree(g_stamps);
+    g_stamps = nullptr;
+    return 0;
+}
+#endif

@@ -674,7 +674,32 @@ static hipError_t fd2_tables(hipStream_t s, const uint4 **out) {
 // the caller's mapped result words and re-zeroes the state block, so a field
 // is ONE launch instead of main + tail + epilogue (under several fields in
 // flight each small launch waited for free CUs: 25-60 us apiece).
+#ifdef NICE_PROBES
+// Probe build: per-workgroup phase stamps (scripts/fd2_stamps.py).  When
+// g_stamps (host, set by nice_probe_fd2_stamps) is non-null, thread 0 of each
+// workgroup b < kStampGroups writes 16 words at stamps + 16 b: for each phase
+// k the constant 100 MHz real-time counter (word 2k) and the shader clock
+// (word 2k + 1).  The stamps go only to that buffer; nothing reads them on
+// the device.
+constexpr u32 kStampGroups = 65536;
+extern u64 *g_stamps;
+#define FD2_STAMP(a, k)                                                               \
+    do {                                                                              \
+        if ((a).stamps && threadIdx.x == 0 && blockIdx.x < kStampGroups) {            \
+            (a).stamps[16 * (u64)blockIdx.x + 2 * (k)] = __builtin_amdgcn_s_memrealtime(); \
+            (a).stamps[16 * (u64)blockIdx.x + 2 * (k) + 1] = __builtin_amdgcn_s_memtime(); \
+        }                                                                             \
+    } while (0)
+#else
+#define FD2_STAMP(a, k) \
+    do {                \
+    } while (0)
+#endif
+
 struct Fd2Args {
+#ifdef NICE_PROBES
+    u64 *stamps;
+#endif
     u64 start_lo, start_hi;
     u64 tail_lo, tail_hi;
     u32 nunits, chunk;
@@ -758,6 +783,7 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
     const u32 chunk = main_part ? a.chunk : 1u;
     const u32 blk = main_part ? blockIdx.x : blockIdx.x - a.main_blocks;
     const u32 nblk = main_part ? a.main_blocks : gridDim.x - a.main_blocks;
+    FD2_STAMP(a, 0);  // start
 
     // The tables (built once per device and base in global memory,
     // fd2_tables) are copied in with 16-byte accesses, and the histogram
@@ -769,6 +795,7 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
         for (u32 i = tid; i < (u32)(P::TB / 16); i += P::WG) h4[i] = make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
+    FD2_STAMP(a, 1);  // tables in LDS
 
     // Window counters: row u - W0, column tid (u32) or tid mod WG/2 (u16 half).
     const u32 hbase = (P::HP ? tid % P::HROW : tid) * 4;
@@ -780,6 +807,7 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
         add_u128(n0_lo, n0_hi, (u64)unit * chunk);
         State<P> st;
         init<P>(st, n0_lo, n0_hi, smem);
+        if (unit == blk * P::WG + tid) FD2_STAMP(a, 2);  // thread 0's first init done
         const u32 r80 = st.r8;
         for (u32 i = 0; i < chunk; i++) {
             u32 m[P::MW], w1 = 0;
@@ -838,7 +866,9 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
         }
     }
     if constexpr ((P::PROBE & 2) != 0) atomicAdd(&outl[P::W0], probe_acc);  // mass only
+    FD2_STAMP(a, 3);  // thread 0's steps done
     __syncthreads();
+    FD2_STAMP(a, 4);  // every wave's steps done
     const u32 lane = tid & 63, wave = tid >> 6;
     u64 *hist_out = a.hist + (blockIdx.x % kHistCopies) * 129;
     for (u32 row = wave; row < (u32)P::W; row += P::WG / 64) {
@@ -854,10 +884,12 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
     }
     if (tid < (u32)P::NBINS && outl[tid])
         atomicAdd((unsigned long long *)&hist_out[tid], (unsigned long long)outl[tid]);
+    FD2_STAMP(a, 5);  // histogram flushed (thread 0's part)
     if (a.fin.out_mapped) {
         __syncthreads();  // smem is reused by the finish
         field_finish<P::WG>(a.fin, a.hist, out.count, smem);
     }
+    FD2_STAMP(a, 6);  // end (the finishing workgroup: after the finish)
 }
 
 template <class P>
@@ -928,6 +960,9 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         const u64 main_blocks = (nunits + P::WG - 1) / P::WG;  // one chunk per lane
         const u64 tail_blocks = (tail + P::WG - 1) / P::WG;
         Fd2Args a{};
+#ifdef NICE_PROBES
+        a.stamps = g_stamps;
+#endif
         a.start_lo = q.start_lo;
         a.start_hi = q.start_hi;
         a.tail_lo = q.start_lo;
