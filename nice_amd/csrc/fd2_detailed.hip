@@ -14,6 +14,7 @@ namespace fd2 {
 
 #ifdef NICE_PROBES
 u64 *g_stamps = nullptr;  // device buffer of the phase stamps (probe build)
+u64 g_last_launch[6] = {};
 #endif
 
 // ---------------------------------------------------------------------------
@@ -192,6 +193,9 @@ hipError_t launch_detailed_fd2(const DetailedLaunch &p, int num_cus, hipStream_t
     u128 a = ((u128)p.start_hi << 64) | p.start_lo;
     const u128 e = a + p.count;
     DetailedLaunch q = p;
+    // p.hist_copies: the same for every launch of the field (enqueue_detailed)
+    if (p.hist_copies < kHistCopies) q.hist_copies = (uint32_t)fd2::probe_knob("NICE_FD2_COPIES", p.hist_copies);
+    if (q.hist_copies < 1 || q.hist_copies > kHistCopies) q.hist_copies = kHistCopies;
     for (size_t i = 0; i <= t.cuts.size() && a < e; i++) {
         u128 stop = i < t.cuts.size() && t.cuts[i] < e ? t.cuts[i] : e;
         if (stop <= a) continue;
@@ -210,11 +214,11 @@ hipError_t launch_detailed_fd2(const DetailedLaunch &p, int num_cus, hipStream_t
 
 #ifdef NICE_PROBES
 // Probe build only: enable (1) the fd2 kernel's per-workgroup phase stamps
-// (kStampGroups x 16 words, zeroed), or read them into out[cap] and disable
+// (kStampGroups x kStampWords words, zeroed), or read them into out[cap] and disable
 // (0).  Synchronous; for scripts/fd2_stamps.py.
 extern "C" int nice_probe_fd2_stamps(int enable, uint64_t *out, size_t cap) {
     using nice::fd2::g_stamps;
-    const size_t words = (size_t)nice::fd2::kStampGroups * 16;
+    const size_t words = (size_t)nice::fd2::kStampGroups * nice::fd2::kStampWords;
     if (enable) {
         if (!g_stamps && hipMalloc(&g_stamps, words * 8) != hipSuccess) return 2;
         return hipMemset(g_stamps, 0, words * 8) == hipSuccess ? 0 : 2;
@@ -225,6 +229,13 @@ extern "C" int nice_probe_fd2_stamps(int enable, uint64_t *out, size_t cap) {
     if (out && n && hipMemcpy(out, g_stamps, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return 2;
     (void)hipFree(g_stamps);
     g_stamps = nullptr;
+    return 0;
+}
+
+// Probe build only: the launch geometry of the last fd2 launch (grid, WG,
+// chunk, nunits, tail, workgroups per CU).
+extern "C" int nice_probe_fd2_last(uint64_t *out6) {
+    for (int k = 0; k < 6; k++) out6[k] = nice::fd2::g_last_launch[k];
     return 0;
 }
 #endif

@@ -136,7 +136,7 @@ constexpr bool fits64(unsigned base, int digits) {
     return true;
 }
 
-template <int BASE_, int ND_, int NE_, int NE2_, int PROBE_ = 0, int WG_ = 512, int VD_ = 0>
+template <int BASE_, int ND_, int NE_, int NE2_, int PROBE_ = 0, int WG_ = 512, int VD_ = 0, int LG_ = -1>
 struct Cfg {
     static constexpr int BASE = BASE_;
     // Bottleneck probes (timing experiments only, results are wrong): 1 = no
@@ -157,7 +157,16 @@ struct Cfg {
     static constexpr int T = log2ceil(B);
     static constexpr u32 BT = (1u << T) - B;
     static constexpr int MW = (BASE + 31) / 32;
-    static constexpr int ES = MW == 1 ? 4 : (MW == 2 ? 8 : 16);  // table entry bytes
+    // VD & 512 (three mask words, b65..68 / b80; probe A/B only): the 80-bit
+    // digit-pair masks SPLIT into an 8-byte table of the digits 0..63
+    // (ds_read_b64) and a u16 table of the digits 64.. (ds_read_u16), both at
+    // an 8-byte stride so one stored limb addresses both through two immediate
+    // offsets.  On uniformly random indices b64 + u16 costs 5.9-6.8 LDS cycles
+    // per wave-lookup against 10.5 for one b128 (scripts/ubench/lds_lookup.hip),
+    // but in the kernel it is 26 % slower on b80 1e9 (9.22 vs 7.31 ms,
+    // profiles/r03/lg_sweep.log): production keeps the 16-byte entries.
+    static constexpr bool SPLIT = MW == 3 && (VD_ & 512) != 0;
+    static constexpr int ES = MW == 1 ? 4 : (MW == 2 || SPLIT ? 8 : 16);  // table entry stride (bytes)
     static constexpr int SH = T + ilog2(ES);                     // carry bit of a scaled limb
     static constexpr u32 ESB = ES * B, EBT = ES * BT;
     static constexpr int WG = WG_;
@@ -169,15 +178,25 @@ struct Cfg {
     // shared by threads t and t + WG/2 when LDS is tight).
     static constexpr int W = window_w(BASE);
     static constexpr int W0 = window_w0(BASE);
-    static constexpr bool HP = true;
-    static constexpr int HROW = HP ? WG / 2 : WG;  // counters per window row
+    // Window counters: HQ per dword (u16 halves shared by threads t and
+    // t + WG/2; SPLIT: u8 quarters, t + k WG/4 -- a lane counts at most one
+    // chunk of <= TCHUNK <= 255 numbers per launch).
+    static constexpr int HQ = SPLIT ? 4 : 2;
+    static constexpr int HROW = WG / HQ;  // counters per window row
     static constexpr int HIST_BYTES = W * HROW * 4;
-    static constexpr int OUTL = HIST_BYTES;  // per-workgroup histogram of out-of-window counts
-    // digit-pair table; at least EBT in: S limbs are stored biased by EBT and
-    // looked up at (TB - EBT) + S, an unsigned immediate offset (b65-68:
-    // EBT ~ 60 KB exceeds the histogram region, so the table starts later)
-    static constexpr int TB0 = (OUTL + 4 * NBINS + 15) / 16 * 16;
-    static constexpr int TB = TB0 >= (int)EBT ? TB0 : ((int)EBT + 15) / 16 * 16;
+    // Layout.  Default: [window rows | out-of-window bins (OUTL) | tables].
+    // The digit-pair table needs at least EBT below it: S limbs are stored
+    // biased by EBT and looked up at (TB - EBT) + S, an unsigned immediate
+    // offset (b65-68: EBT exceeds the histogram region, so the table starts
+    // later).  SPLIT: [OUTL | pad | X1 at TB = EBT | X2 at TH | window rows]:
+    // the C limbs (unbiased) reach X2 at TH + C, so TH < 65536; X2 starts one
+    // entry before X1 ends (TB + 8B = 8 * 2^T = 65536), where both tables hold
+    // zeros (X1's last entry marks only digits >= 64, X2's first none).
+    static constexpr int TB0 = SPLIT ? 0 : (HIST_BYTES + 4 * NBINS + 15) / 16 * 16;
+    static constexpr int TB = SPLIT ? (int)EBT : (TB0 >= (int)EBT ? TB0 : ((int)EBT + 15) / 16 * 16);
+    static constexpr int TH = TB + (int)(B * ES) - ES;  // SPLIT: X2, the u16 high words
+    static constexpr int OUTL = SPLIT ? 0 : HIST_BYTES;  // per-workgroup histogram of out-of-window counts
+    static constexpr int TC0 = TB / 16 * 16;  // the table image starts here (16-byte copy)
     // Low-digit entry, word 1: digit bits [0, DB), then the carries and flags
     // of the step n -> n+1, all functions of n mod B (limb 0 of S, C, D1, N3
     // is never stored): the carry out of S limb 0 of S += D1 and the carry
@@ -192,8 +211,12 @@ struct Cfg {
     static constexpr bool LSD = MW == 2 && DB > 0 && DB + (TIGHT ? 4 : 10) <= 30;
     // (regions padded to 16 bytes: the image is copied in with 16-byte accesses)
     static constexpr int TL = TB + ((int)(B * ES) + 15) / 16 * 16;  // low-digit table (2B entries)
-    static constexpr int LDS_BYTES = TL + (LSD ? ((int)(2 * B * ES) + 15) / 16 * 16 : 0);
-    static constexpr int TAB_BYTES = LDS_BYTES - TB;  // table image copied in per workgroup
+    static constexpr int TEND = SPLIT ? (TH + (int)(B * ES) + 15) / 16 * 16
+                                      : TL + (LSD ? ((int)(2 * B * ES) + 15) / 16 * 16 : 0);
+    static constexpr int HB = SPLIT ? TEND : 0;  // window rows
+    static constexpr int LDS_BYTES = SPLIT ? HB + HIST_BYTES : TEND;
+    static constexpr int TAB_BYTES = TEND - TC0;  // table image copied in per workgroup
+    static constexpr int ZA = SPLIT ? TC0 : TB;   // zeroed per workgroup: [0, ZA) and [HB, LDS_BYTES)
     static constexpr int LO = LSD ? 1 : 0;  // first stored / looked-up limb
     static constexpr u32 DMASK = (1u << (DB > 0 && DB < 32 ? DB : 0)) - 1;
     static constexpr u32 FLAG_D1 = 1u << 30, FLAG_N3 = 1u << 31;  // any flag: w1 >= FLAG_D1
@@ -218,13 +241,21 @@ struct Cfg {
     // MW = 3) for one data-random (bank-conflicting) LDS read.
     static constexpr int VD = VD_;
     static constexpr int VDC = VD % 16, VDS = (VD / 16) % 16;
+    // Lookup groups: a scheduling barrier after every LG table lookups of a
+    // step (0: none), so the compiler cannot hoist all of a step's LDS reads
+    // ahead of their ORs -- with SPLIT's b64 + u16 pairs that held ~75 VGPRs
+    // of loaded words at once and spilled the 1024-thread b80 kernel at its
+    // 128-VGPR budget; the 16-byte layout spilled 52-64 bytes per lane there
+    // too, and LG 8 removes it (b80 1e9 7.45 -> 7.31 ms, lg_sweep.log).
+    // -1: the per-base default.
+    static constexpr int LG = LG_ >= 0 ? LG_ : (MW == 3 && WG >= 1024 ? 8 : 0);
     // VD & 256 (no low-digit table only): limb 0 of S and of C by VALU too --
     // n^2 mod B and n^3 mod B of a wave's lanes keep few residues mod 16, so
     // their lookups pile onto few bank quads
     static constexpr bool VDL = (VD & 256) != 0 && !LSD;
     static constexpr u32 MAGIC_D = (u32)(((1ull << 32) + ES * BASE - 1) / (ES * BASE));
     static_assert(VD == 0 || (MW >= 2 && split_exact(BASE, ES, MAGIC_D)), "VALU digit split");
-    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1 && (VD & ~0x1ff) == 0,
+    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1 && (VD & ~0x3ff) == 0,
                   "VALU-decoded limbs");
     // Waves per SIMD: what the LDS allows, capped by what the lane state
     // needs in VGPRs (the register budget is set to match, see state_waves).
@@ -237,8 +268,10 @@ struct Cfg {
     static_assert(ND <= NX + 1 && NE2 <= NX + 1 && NE <= NS + 1, "difference limb counts");
     static_assert(S_TOPD >= 1 && C_TOPD >= 1, "top limb");
     static_assert(TB >= (int)EBT && TB - (int)EBT < 65536 && (!LSD || TL < 65536), "LDS offsets");
+    static_assert(!SPLIT || (TH < 65536 && TB + (int)(B * ES) == ES << T && 4 * NBINS <= TC0 && TCHUNK <= 255),
+                  "split layout");
     static_assert(LDS_BYTES <= 163840, "LDS");
-    static_assert(TB % 16 == 0 && TAB_BYTES % 16 == 0, "16-byte table copy");
+    static_assert((SPLIT || TB % 16 == 0) && TAB_BYTES % 16 == 0 && HB % 16 == 0, "16-byte table copy");
     static_assert(W0 >= 0 && W0 + W <= NBINS, "window");
     static_assert(!LSD || (ES == 8 && FC + FCW <= 30), "low-digit entry layout");
     static_assert(C1 || ((unsigned long long)MAGICB * B - (1ull << 32)) * (TMAX / ES) < (1ull << 32),
@@ -283,6 +316,12 @@ __device__ __forceinline__ void or_entry(const unsigned char *p, u32 (&m)[P::MW]
         uint2 v = *(const uint2 *)p;
         m[0] |= v.x;
         m[1] |= v.y;
+    } else if constexpr (P::SPLIT) {
+        // the same stored limb addresses both tables (two immediate offsets)
+        uint2 v = *(const uint2 *)p;
+        m[0] |= v.x;
+        m[1] |= v.y;
+        m[2] |= *(const unsigned short *)(p + (P::TH - P::TB));
     } else {
         uint4 v = *(const uint4 *)p;
         m[0] |= v.x;
@@ -293,6 +332,17 @@ __device__ __forceinline__ void or_entry(const unsigned char *p, u32 (&m)[P::MW]
         // over 32 banks (8 cycles per wave) instead of 4 groups over 64 (4).
         asm volatile("" ::"v"(v.w));
     }
+}
+
+// End of a lookup group (Cfg::LG): the group's ORs are pinned here (the mask
+// words pass through an empty asm, so LLVM cannot re-associate every OR of a
+// step into one tree at its end) and no instruction crosses the point, so
+// the group's loaded words are dead before the next group's reads issue.
+template <class P>
+__device__ __forceinline__ void lookup_group_end(u32 (&m)[P::MW]) {
+#pragma unroll
+    for (int w = 0; w < P::MW; w++) asm volatile("" : "+v"(m[w]));
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // Digit bits of a scaled limb (vs = ES v, v < B) by VALU: the high digit by
@@ -362,8 +412,10 @@ __device__ __forceinline__ void normalize(const A (&acc)[N], u32 (&out)[M]) {
     }
 }
 
+// Lane state at n (every limb but the cached mask, which needs the tables:
+// recompute_hi after them).
 template <class P>
-__device__ __forceinline__ void init(State<P> &st, u64 n_lo, u64 n_hi, const unsigned char *smem) {
+__device__ __forceinline__ void init(State<P> &st, u64 n_lo, u64 n_hi) {
     constexpr u32 B = P::B;
     u32 X[P::NX];
     if constexpr (P::N64) {
@@ -468,7 +520,6 @@ __device__ __forceinline__ void init(State<P> &st, u64 n_lo, u64 n_hi, const uns
             normalize<P>(acc, st.N3);
         }
     }
-    recompute_hi<P>(st, smem);
     if constexpr (P::LSD) st.S[0] = st.C[0] = st.D1[0] = st.N3[0] = 0;  // from the table
 #pragma unroll
     for (int i = 0; i < P::SL; i++) st.S[i] = (st.S[i] + P::BT) * P::ES;
@@ -622,7 +673,13 @@ __global__ void fd2_tables_kernel(unsigned char *tb) {
         else *(uint4 *)p = make_uint4(v[0], v[1], v[2], v[3]);
     };
     mark(e);
-    put(tb + e * P::ES);
+    put(tb + (P::TB - P::TC0) + e * P::ES);
+    if constexpr (P::SPLIT) {
+        // X2: the u16 high word (digits 64..) at the same stride; its entry 0
+        // shares its bytes with X1's last entry, zero in both (static_assert)
+        static_assert(P::BASE <= 80, "X2 holds the digits 64..79");
+        if (v[2]) *(unsigned short *)(tb + (P::TH - P::TC0) + e * P::ES) = (unsigned short)v[2];
+    }
     if constexpr (P::LSD) {
         v[0] = v[1] = v[2] = v[3] = 0;
         const u32 B = P::B;
@@ -677,20 +734,26 @@ static hipError_t fd2_tables(hipStream_t s, const uint4 **out) {
 #ifdef NICE_PROBES
 // Probe build: per-workgroup phase stamps (scripts/fd2_stamps.py).  When
 // g_stamps (host, set by nice_probe_fd2_stamps) is non-null, thread 0 of each
-// workgroup b < kStampGroups writes 16 words at stamps + 16 b: for each phase
-// k the constant 100 MHz real-time counter (word 2k) and the shader clock
-// (word 2k + 1).  The stamps go only to that buffer; nothing reads them on
-// the device.
-constexpr u32 kStampGroups = 65536;
+// workgroup b < kStampGroups writes kStampWords words at stamps + kStampWords b:
+// for each phase k the constant 100 MHz real-time counter (word 2k) and the
+// shader clock (word 2k + 1).  The stamps go only to that buffer; nothing
+// reads them on the device.  Phases 7..9 are the finishing workgroup's
+// field finish.
+constexpr u32 kStampGroups = 65536, kStampWords = 32;
 extern u64 *g_stamps;
-#define FD2_STAMP(a, k)                                                               \
-    do {                                                                              \
-        if ((a).stamps && threadIdx.x == 0 && blockIdx.x < kStampGroups) {            \
-            (a).stamps[16 * (u64)blockIdx.x + 2 * (k)] = __builtin_amdgcn_s_memrealtime(); \
-            (a).stamps[16 * (u64)blockIdx.x + 2 * (k) + 1] = __builtin_amdgcn_s_memtime(); \
-        }                                                                             \
+extern u64 g_last_launch[6];  // grid, WG, chunk, nunits, tail, per_cu of the last launch
+#define FD2_STAMP_P(p, k)                                                                        \
+    do {                                                                                         \
+        if ((p) && threadIdx.x == 0 && blockIdx.x < kStampGroups) {                              \
+            (p)[kStampWords * (u64)blockIdx.x + 2 * (k)] = __builtin_amdgcn_s_memrealtime();     \
+            (p)[kStampWords * (u64)blockIdx.x + 2 * (k) + 1] = __builtin_amdgcn_s_memtime();     \
+        }                                                                                        \
     } while (0)
+#define FD2_STAMP(a, k) FD2_STAMP_P((a).stamps, k)
 #else
+#define FD2_STAMP_P(p, k) \
+    do {                  \
+    } while (0)
 #define FD2_STAMP(a, k) \
     do {                \
     } while (0)
@@ -705,6 +768,7 @@ struct Fd2Args {
     u32 nunits, chunk;
     u32 tail_count, main_blocks;
     u32 cutoff;
+    u32 ncopies;        // histogram copies in use (<= kHistCopies), the same for every launch of a field
     u64 *hist;          // kHistCopies x 129 bins
     NumOut out;
     const uint4 *tabs;
@@ -720,20 +784,23 @@ struct Fd2Args {
 // here would write back and invalidate the XCD's whole L2 once per
 // workgroup: 12 000 of them made the b40 1e9 field 1.8x slower.
 template <int WG>
-__device__ __forceinline__ void field_finish(const FieldFinish &fin, u64 *hist, u32 *count,
-                                             unsigned char *smem) {
+__device__ __forceinline__ void field_finish(const FieldFinish &fin, u64 *hist, u32 ncopies, u32 *count,
+                                             unsigned char *smem, u64 *stamps) {
+    (void)stamps;
     __shared__ u32 last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) last = last_block_arrive(fin.done);
     __syncthreads();
     if (!last) return;
+    FD2_STAMP_P(stamps, 7);  // the last workgroup: arrival known
     unsigned long long *acc = (unsigned long long *)smem;
     for (u32 b = threadIdx.x; b < 129; b += WG) acc[b] = 0;
     __syncthreads();
     // All of a lane's loads issued before the first is used: one L2 round
-    // trip for the 64 x 129 copies instead of one per copy row.
-    constexpr u32 NE = kHistCopies * 129, PER = (NE + WG - 1) / WG;
+    // trip for the ncopies x 129 copies instead of one per copy row.
+    constexpr u32 PER = (kHistCopies * 129 + WG - 1) / WG;
+    const u32 NE = ncopies * 129;
     const u32 nmiss = threadIdx.x == 0 ? __hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
     u64 v[PER];
 #pragma unroll
@@ -750,6 +817,7 @@ __device__ __forceinline__ void field_finish(const FieldFinish &fin, u64 *hist, 
         }
     }
     __syncthreads();
+    FD2_STAMP_P(stamps, 8);  // copies read and summed
     for (u32 b = threadIdx.x; b < 129; b += WG) fin.out_mapped[b] = acc[b];
     if (threadIdx.x == 0) {
         fin.out_mapped[129] = nmiss;
@@ -761,6 +829,7 @@ __device__ __forceinline__ void field_finish(const FieldFinish &fin, u64 *hist, 
     // write-back costs nothing measurable).
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    FD2_STAMP_P(stamps, 9);  // mapped stores complete
     if (threadIdx.x == 0)
         __hip_atomic_store(&fin.out_mapped[130], fin.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -770,7 +839,7 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
     // Static LDS: its address is a compile-time constant, so a lookup is one
     // ds_read with the table offset in the instruction's immediate field.
     __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDS_BYTES];
-    u32 *hist = (u32 *)smem;
+    u32 *hist = (u32 *)(smem + P::HB);
     u32 *outl = (u32 *)(smem + P::OUTL);
     const u32 tid = threadIdx.x;
     const NumOut out = a.out;
@@ -782,32 +851,49 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
     const u32 nunits = main_part ? a.nunits : a.tail_count;
     const u32 chunk = main_part ? a.chunk : 1u;
     const u32 blk = main_part ? blockIdx.x : blockIdx.x - a.main_blocks;
-    const u32 nblk = main_part ? a.main_blocks : gridDim.x - a.main_blocks;
     FD2_STAMP(a, 0);  // start
 
     // The tables (built once per device and base in global memory,
-    // fd2_tables) are copied in with 16-byte accesses, and the histogram
-    // region zeroed: building them here cost ~5 % of a launch of short chunks.
+    // fd2_tables) are DMA'd into LDS, and the histogram region zeroed:
+    // building them here cost ~5 % of a launch of short chunks.  One
+    // global_load_lds_dwordx4 wave-instruction moves 1 KiB (lane l's 16 bytes
+    // land at the wave-uniform base + 16 l): every load of the copy is in
+    // flight at once, with no VGPR round trip and no ds_write (the register
+    // copy it replaces waited one L2 round trip per 16 bytes a lane moved:
+    // b40 1e6 spent 2.1 us of a 12.5 us kernel in it, fd2_stamps_before.log).
     {
-        uint4 *dst = (uint4 *)(smem + P::TB);
-        for (u32 i = tid; i < (u32)(P::TAB_BYTES / 16); i += P::WG) dst[i] = a.tabs[i];
+        constexpr u32 N16 = (u32)(P::TAB_BYTES / 16);
+        const u32 lane = tid & 63, w64 = tid & ~63u;
+        for (u32 i0 = w64; i0 < N16; i0 += P::WG)
+            if (i0 + lane < N16)
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(a.tabs + i0 + lane),
+                                                 (__attribute__((address_space(3))) void *)(smem + P::TC0 + 16 * i0),
+                                                 16, 0, 0);
         uint4 *h4 = (uint4 *)smem;
-        for (u32 i = tid; i < (u32)(P::TB / 16); i += P::WG) h4[i] = make_uint4(0, 0, 0, 0);
+        for (u32 i = tid; i < (u32)(P::ZA / 16); i += P::WG) h4[i] = make_uint4(0, 0, 0, 0);
+        if constexpr (P::SPLIT)
+            for (u32 i = tid; i < (u32)(P::HIST_BYTES / 16); i += P::WG)
+                h4[P::HB / 16 + i] = make_uint4(0, 0, 0, 0);
     }
-    __syncthreads();
-    FD2_STAMP(a, 1);  // tables in LDS
+    // A lane takes at most ONE chunk (launch_cfg sizes the grid to cover every
+    // unit), so its state is built while the table DMA is in flight; only the
+    // cached high limbs' mask needs the tables.
+    const u32 unit = blk * P::WG + tid;
+    const bool active = unit < nunits;
+    u64 n0_lo = start_lo, n0_hi = start_hi;
+    add_u128(n0_lo, n0_hi, (u64)unit * chunk);
+    State<P> st;
+    if (active) init<P>(st, n0_lo, n0_hi);
+    __syncthreads();  // drains the DMA (vmcnt(0)) before the barrier
+    FD2_STAMP(a, 1);  // state built, tables in LDS
 
-    // Window counters: row u - W0, column tid (u32) or tid mod WG/2 (u16 half).
-    const u32 hbase = (P::HP ? tid % P::HROW : tid) * 4;
-    const u32 hinc = P::HP && tid >= (u32)P::HROW ? 0x10000u : 1u;
-    const u32 stride = nblk * P::WG;
+    // Window counters: row u - W0, column tid mod HROW (u16 halves / u8 quarters).
+    const u32 hbase = P::HB + tid % P::HROW * 4;
+    const u32 hinc = 1u << (32 / P::HQ * (tid / P::HROW));
     u32 probe_acc = 0;
-    for (u32 unit = blk * P::WG + tid; unit < nunits; unit += stride) {
-        u64 n0_lo = start_lo, n0_hi = start_hi;
-        add_u128(n0_lo, n0_hi, (u64)unit * chunk);
-        State<P> st;
-        init<P>(st, n0_lo, n0_hi, smem);
-        if (unit == blk * P::WG + tid) FD2_STAMP(a, 2);  // thread 0's first init done
+    if (active) {
+        recompute_hi<P>(st, smem);
+        FD2_STAMP(a, 2);  // thread 0's cached mask done
         const u32 r80 = st.r8;
         for (u32 i = 0; i < chunk; i++) {
             u32 m[P::MW], w1 = 0;
@@ -832,12 +918,14 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
                     if ((P::PROBE & 4) && q == 1) { m[0] |= st.S[q] & 0xffu; continue; }  // probe: no limb-1 lookups
                     if (q >= P::SL - P::VDS || (P::VDL && q == 0)) or_valu<P>(st.S[q] - P::EBT, m);
                     else or_entry<P>(smem + (P::TB - P::EBT) + st.S[q], m);
+                    if (P::LG && (q - P::LO + 1) % P::LG == 0) lookup_group_end<P>(m);
                 }
 #pragma unroll
                 for (int q = P::LO; q < P::CL; q++) {
                     if ((P::PROBE & 4) && q == 1) { m[1] |= st.C[q] & 0xffu; continue; }
                     if (q >= P::CL - P::VDC || (P::VDL && q == 0)) or_valu<P>(st.C[q], m);
                     else or_entry<P>(smem + P::TB + st.C[q], m);
+                    if (P::LG && (P::SL + q - 2 * P::LO + 1) % P::LG == 0) lookup_group_end<P>(m);
                 }
             }
             // uw = unique count - W0: the bias rides in the first v_bcnt's
@@ -870,24 +958,45 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
     __syncthreads();
     FD2_STAMP(a, 4);  // every wave's steps done
     const u32 lane = tid & 63, wave = tid >> 6;
-    u64 *hist_out = a.hist + (blockIdx.x % kHistCopies) * 129;
-    for (u32 row = wave; row < (u32)P::W; row += P::WG / 64) {
+    u64 *hist_out = a.hist + (blockIdx.x % a.ncopies) * 129;
+    // Window rows: wave w sums rows w, w + WG/64, ...; all of a wave's rows
+    // are read and reduced together, so their cross-lane steps overlap.
+    constexpr u32 NWAVE = P::WG / 64, RPW = (P::W + NWAVE - 1) / NWAVE;
+    u32 rs[RPW];
+#pragma unroll
+    for (u32 k = 0; k < RPW; k++) {
+        const u32 row = wave + k * NWAVE;
         u32 s = 0;
+        if (row < (u32)P::W) {
 #pragma unroll
-        for (int q = 0; q < P::HROW / 64; q++) {
-            const u32 v = hist[row * P::HROW + lane + 64 * q];
-            s += P::HP ? (v & 0xffffu) + (v >> 16) : v;
+            for (int q = 0; q < P::HROW / 64; q++) {
+                const u32 v = hist[row * P::HROW + lane + 64 * q];
+                if constexpr (P::HQ == 2) s += (v & 0xffffu) + (v >> 16);
+                else s += (v & 0xffu) + ((v >> 8) & 0xffu) + ((v >> 16) & 0xffu) + (v >> 24);
+            }
         }
+        rs[k] = s;
+    }
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
-        if (lane == 0 && s) atomicAdd((unsigned long long *)&hist_out[P::W0 + row], (unsigned long long)s);
+    for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+        for (u32 k = 0; k < RPW; k++) rs[k] += __shfl_xor(rs[k], o);
+#pragma unroll
+    for (u32 k = 0; k < RPW; k++) {
+        const u32 row = wave + k * NWAVE;
+        if (lane == 0 && row < (u32)P::W && rs[k])
+            atomicAdd((unsigned long long *)&hist_out[P::W0 + row], (unsigned long long)rs[k]);
     }
     if (tid < (u32)P::NBINS && outl[tid])
         atomicAdd((unsigned long long *)&hist_out[tid], (unsigned long long)outl[tid]);
     FD2_STAMP(a, 5);  // histogram flushed (thread 0's part)
     if (a.fin.out_mapped) {
         __syncthreads();  // smem is reused by the finish
-        field_finish<P::WG>(a.fin, a.hist, out.count, smem);
+#ifdef NICE_PROBES
+        field_finish<P::WG>(a.fin, a.hist, a.ncopies, out.count, smem, a.stamps);
+#else
+        field_finish<P::WG>(a.fin, a.hist, a.ncopies, out.count, smem, nullptr);
+#endif
     }
     FD2_STAMP(a, 6);  // end (the finishing workgroup: after the finish)
 }
@@ -913,8 +1022,10 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
     hipError_t e = hipSuccess;
     // Resident lanes (one "round" of workgroups).
     const u64 lanes = (u64)num_cus * per_cu * P::WG;
-    // u16 counters: at most 65535 numbers per lane per launch.
-    const u64 max_count = P::HP ? lanes * 60000ull : ~0ull;
+    // Launch size bound (nunits fits 32 bits).  A lane takes ONE chunk per
+    // launch, so its window counters count at most chunk <= TCHUNK numbers
+    // (u16 halves; u8 quarters need chunk <= 255, checked below).
+    const u64 max_count = lanes * 60000ull;
     // Every near-miss count must lie above the window (it is recorded on the
     // out-of-window branch).
     if (p.cutoff + 1 < (u32)(P::W0 + P::W)) return hipErrorInvalidValue;
@@ -952,8 +1063,9 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         // pair table, and a chunk divisible by 16 puts a 16-lane group on
         // ONE bank quad for those lookups (n^2 mod 16 equal on every lane):
         // b80 1e9 at chunk 2544 took 11.8 ms, at 2545 9.3.
-        if (chunk > 1 && chunk % 2 == 0) chunk++;
+        if (chunk > 1 && (P::LSD ? chunk % 2 == 0 : chunk % 16 == 0)) chunk++;
         if (chunk > P::B) chunk = P::B % 2 ? P::B : P::B - 1;
+        if (P::HQ == 4 && chunk > 255) return hipErrorInvalidValue;
         const u64 nunits = cnt / chunk;
         if (nunits > 0xffffffffull) return hipErrorInvalidValue;
         const u64 tail = cnt - nunits * chunk;  // < chunk <= B: one number per lane
@@ -973,11 +1085,18 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         a.tail_count = (u32)tail;
         a.main_blocks = (u32)main_blocks;
         a.cutoff = q.cutoff;
+        a.ncopies = q.hist_copies;
         a.hist = q.hist;
         a.out = q.out;
         a.tabs = tabs;
         // the field's finish rides on its last launch
         a.fin = left == cnt ? q.fin : FieldFinish{nullptr, nullptr};
+#ifdef NICE_PROBES
+        {
+            const u64 v[6] = {main_blocks + tail_blocks, (u64)P::WG, chunk, nunits, tail, (u64)per_cu};
+            for (int k = 0; k < 6; k++) g_last_launch[k] = v[k];
+        }
+#endif
         hipLaunchKernelGGL(kern, dim3((u32)(main_blocks + tail_blocks)), dim3(P::WG), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         add_u128(q.start_lo, q.start_hi, cnt);
@@ -997,10 +1116,10 @@ namespace fd2 {
 // formulas of Cfg, evaluated without instantiating it).
 constexpr int lds_bytes(int base, int wg) {
     const int mw = (base + 31) / 32, es = mw == 1 ? 4 : (mw == 2 ? 8 : 16), b2 = base * base;
-    const int tb0 = (window_w(base) * (wg / 2) * 4 + 4 * (base + 1) + 15) / 16 * 16;
     int t = 0;
     while ((1 << t) < b2) t++;
     const int ebt = es * ((1 << t) - b2);
+    const int tb0 = (window_w(base) * (wg / 2) * 4 + 4 * (base + 1) + 15) / 16 * 16;
     const int tb = tb0 >= ebt ? tb0 : (ebt + 15) / 16 * 16;
     const int db = base - 32;
     const bool lsd = mw == 2 && db > 0 && db + (db > 20 ? 4 : 10) <= 30;

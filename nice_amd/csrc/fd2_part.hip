@@ -22,6 +22,11 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
         return hipErrorNotFound;
     } else {
         if ((int)p.base != B_ || nd != ND_ || ne != NE_ || ne2 != NE2_) return hipErrorNotFound;
+        // the host's occupancy model (big_wg) reads the same layout
+        static_assert(Cfg<B_, ND_, NE_, NE2_, 0, 512, valu_limbs(B_)>::LDS_BYTES == lds_bytes(B_, 512) &&
+                          Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), valu_limbs(B_)>::LDS_BYTES ==
+                              lds_bytes(B_, big_wg(B_)),
+                      "lds_bytes mirrors Cfg");
 #ifdef NICE_PROBES
         // VALU-decoded limb sweep (scripts/vd_sweep.py): NICE_FD2_VD = 100 + VD
         switch ((int)probe_knob("NICE_FD2_VD", 0)) {
@@ -35,6 +40,22 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
         case 357: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 257>>(p, num_cus, s);
         case 358: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 258>>(p, num_cus, s);
         default: break;
+        }
+        // Lookup-group sweep of the three-mask-word bases (NICE_FD2_LG = LG,
+        // or 1000 + LG: the split b64 + u16 layout with that grouping)
+        if constexpr ((B_ + 31) / 32 == 3) {
+            constexpr int VL = valu_limbs(B_), WGB = big_wg(B_);
+            switch ((int)probe_knob("NICE_FD2_LG", 100000)) {
+            case 0: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL, 0>>(p, num_cus, s);
+            case 6: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL, 6>>(p, num_cus, s);
+            case 8: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL, 8>>(p, num_cus, s);
+            case 12: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL, 12>>(p, num_cus, s);
+            case 16: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL, 16>>(p, num_cus, s);
+            case 1000: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL | 512, 0>>(p, num_cus, s);
+            case 1008: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL | 512, 8>>(p, num_cus, s);
+            case 1012: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL | 512, 12>>(p, num_cus, s);
+            default: break;
+            }
         }
 #endif
         return wg512 ? launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, valu_limbs(B_)>>(p, num_cus, s)

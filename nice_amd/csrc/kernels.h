@@ -37,6 +37,7 @@ struct DetailedLaunch {
     uint32_t base;
     uint32_t cutoff;             // near-miss cutoff (number_stats.rs:15-17)
     uint64_t *hist;              // kHistCopies x 129 u64 bins, accumulated
+    uint32_t hist_copies;        // fd2: copies the field's launches use (set by launch_detailed_fd2)
     NumOut out;
     FieldFinish fin;             // fd2 only; see FieldFinish
 };

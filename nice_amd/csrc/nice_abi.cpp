@@ -504,6 +504,11 @@ int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *f
     u128 rs = 0, re = 0;
     const bool fd_base = nice::fd2_supported(base);
     const bool fd = fd_base && nice::base_range_cached(base, rs, re) == 1;
+    // Histogram copies the field's launches flush into: a small field run
+    // wholly by fd2 keeps 16 (its whole grid flushes at once, and the
+    // in-kernel finish reads every copy in use); anything else all 64 (the
+    // generic kernel and the finish kernel use all of them).
+    p.hist_copies = fd && s >= rs && e <= re && e - s < 20000000 ? 16 : nice::kHistCopies;
     if (!fd) return launch(s, e, false);
     int rc;
     if ((rc = launch(s, std::min(e, rs), false))) return rc;
