@@ -417,6 +417,29 @@ def test_size_independent_properties(ctx):
     assert ctx.detailed_raw(s, e, 40) == (h, l)
 
 
+@pytest.mark.parametrize("base", [40, 65, 67, 68, 80])
+def test_big_field_kernel_equals_small_field_kernel(ctx, base):
+    """Fields >= 1e7 run the big-field instantiation (1024-thread workgroups,
+    the three-mask-word bases with lookup groups, 64 histogram copies); fields
+    < 1e7 the 512-thread one (16 copies), pinned against the oracle by
+    test_fd_kernel_production_bases.  A 2e7 window 1/4 into the range must
+    equal the sum of its twenty 1e6 sub-windows (histogram) and their
+    concatenation (near-miss list); every near-miss recomputes by the oracle."""
+    r0, r1 = O.base_range(base)
+    s = r0 + (r1 - r0) // 4
+    h, l = ctx.detailed_raw(s, s + 2 * 10 ** 7, base)
+    assert sum(h) == 2 * 10 ** 7
+    hs, ls = [0] * len(h), []
+    for k in range(20):
+        a = s + k * 10 ** 6
+        hk, lk = ctx.detailed_raw(a, a + 10 ** 6, base)
+        hs = [x + y for x, y in zip(hs, hk)]
+        ls += lk
+    assert h == hs and l == ls
+    assert sum(h[O.near_miss_cutoff(base) + 1:]) == len(l)
+    assert all(O.num_unique_digits(n, base) == u for n, u in l)
+
+
 def test_multi_device_context_sharding():
     import torch
     n = torch.cuda.device_count()
