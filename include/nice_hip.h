@@ -74,7 +74,16 @@ int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start
  * candidate set identical to process_range_niceonly's):
  *   msd_floor  MSD recursion floor; 0 -> NICE_GPU_MSD_FLOOR from the
  *              environment when set to a number >= 1 (the reference's pin,
- *              client_process_gpu.rs:161-172), else 250 (msd_prefix_filter.rs:282)
+ *              client_process_gpu.rs:161-172), else 250 (msd_prefix_filter.rs:282);
+ *              NICE_MSD_FLOOR_ADAPTIVE -> the reference GPU path's adaptive
+ *              floor (AdaptiveFloor, client_process_gpu.rs:96-184, 551-568):
+ *              process-wide, pinned by NICE_GPU_MSD_FLOOR, else seeded at
+ *              512 000 / logical cores in [250, 256 000]; after 3 warmup
+ *              fields every host-MSD field moves it by msd / gpu-tail time
+ *              (nice_adaptive_floor_step).  Device-MSD fields use it without
+ *              updating it: their recursion is not a host phase to balance.
+ *              A floor above 250 checks a superset of the candidates; the
+ *              nice list is unchanged.
  *   chunk_size MSD chunking of the field; 0 -> reference client rule
  *              1e6 * clamp(ceil(size / 1e11), 1, 1000) (client/src/main.rs:158-168)
  *   threads    host MSD worker threads; 0 -> hardware concurrency
@@ -90,6 +99,7 @@ int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start
  *              reference deals descriptors from a shared channel,
  *              client_process_gpu.rs:589-709).
  * Both MSD placements produce the same candidate set. */
+#define NICE_MSD_FLOOR_ADAPTIVE UINT64_MAX
 #define NICE_MSD_AUTO 0
 #define NICE_MSD_HOST 1
 #define NICE_MSD_DEVICE 2
@@ -114,7 +124,17 @@ typedef struct {
                                mod 2^32; 0 where not counted (host MSD, other bases) */
     double msd_seconds;     /* until the last MSD worker finished */
     double total_seconds;
+    uint64_t msd_floor;     /* the MSD recursion floor this field used */
 } nice_niceonly_stats;
+
+/* AdaptiveFloor::update's step (client_process_gpu.rs:130-157): the floor
+ * after a field whose MSD took msd_seconds of total_seconds -- ratio
+ * msd / (total - msd), 1.5 when the GPU tail is under 2 ms, 1/1.5 when the
+ * MSD is, clamped to [1/1.5, 1.5], the floor to [250, 256 000].  Pure. */
+double nice_adaptive_floor_step(double floor, double msd_seconds, double total_seconds);
+/* The process-wide adaptive floor now, and the warmup fields left
+ * (0xffffffff: pinned by NICE_GPU_MSD_FLOOR). */
+int nice_adaptive_floor(double *floor, uint32_t *warmup);
 
 /* process_range_niceonly_gpu(&GpuContext, &FieldSize, base) -> FieldResults
  * (client_process_gpu.rs:515-557; CPU semantics client_process.rs:439-465).

@@ -6,7 +6,7 @@ package is the host-side mirror of the reference's API for that path.
 """
 from ._lib import NiceError, NiceLibraryError, build, lib  # noqa: F401
 from .api import (CLIENT_VERSION, GPU_BATCH_SIZE, PROCESSING_CHUNK_SIZE, BothModes,  # noqa: F401
-                  GpuContext, StrideTable, default_context, get_base_range_u128, get_near_miss_cutoff,
+                  GpuContext, adaptive_floor, adaptive_floor_step, StrideTable, default_context, get_base_range_u128, get_near_miss_cutoff,
                   get_valid_ranges, gpu_supports_base, has_duplicate_msd_prefix,
                   process_detailed_gpu, process_niceonly_gpu, process_range_detailed,
                   process_range_detailed_gpu, process_range_niceonly,

@@ -19,6 +19,7 @@ NICE_ERR_HIP = 2
 NICE_ERR_CAPACITY = 3
 NICE_ERR_NO_DEVICE = 4
 NICE_ERR_MSD_OVERFLOW = 5
+NICE_MSD_FLOOR_ADAPTIVE = (1 << 64) - 1  # msd_floor: the reference GPU path's AdaptiveFloor
 
 # Every symbol include/nice_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -32,6 +33,7 @@ EXPORTS = (
     "nice_fd_segment_cuts", "nice_validate_detailed", "nice_detailed_submit",
     "nice_detailed_collect", "nice_niceonly_submit", "nice_niceonly_collect",
     "nice_cpu_process_range_detailed", "nice_cpu_process_range_niceonly",
+    "nice_adaptive_floor_step", "nice_adaptive_floor",
 )
 
 
@@ -61,7 +63,7 @@ class nice_niceonly_stats(ctypes.Structure):
     _fields_ = [("ranges", ctypes.c_uint64), ("range_numbers", ctypes.c_uint64),
                 ("candidates", ctypes.c_uint64), ("launches", ctypes.c_uint32),
                 ("square_ok", ctypes.c_uint32), ("msd_seconds", ctypes.c_double),
-                ("total_seconds", ctypes.c_double)]
+                ("total_seconds", ctypes.c_double), ("msd_floor", ctypes.c_uint64)]
 
 
 class nice_kernel_stats(ctypes.Structure):
@@ -131,6 +133,8 @@ def lib():
         "nice_niceonly_collect": ([vp, i32, PN, sz, PSZ, ctypes.POINTER(nice_niceonly_stats)], i32),
         "nice_cpu_process_range_detailed": ([u64, u64, u64, u64, u32, i32, P64, PN, sz, PSZ], i32),
         "nice_cpu_process_range_niceonly": ([u64, u64, u64, u64, u32, u32, i32, PN, sz, PSZ], i32),
+        "nice_adaptive_floor_step": ([ctypes.c_double, ctypes.c_double, ctypes.c_double], ctypes.c_double),
+        "nice_adaptive_floor": ([ctypes.POINTER(ctypes.c_double), P32], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -12,7 +12,7 @@ from __future__ import annotations
 import ctypes
 import threading
 from dataclasses import dataclass
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 from . import _lib
 from ._lib import check, lib
@@ -111,6 +111,27 @@ class NiceonlyStats:
     # device MSD, in-range fast bases: candidates whose square alone has no
     # repeated digit (mod 2^32; 0 where not counted)
     square_ok: int = 0
+    # the MSD recursion floor the field used (msd_floor="adaptive": the
+    # adaptive floor's value at submit)
+    msd_floor: int = 0
+
+
+def _stats(st) -> NiceonlyStats:
+    return NiceonlyStats(st.ranges, st.range_numbers, st.candidates, st.launches,
+                         st.msd_seconds, st.total_seconds, st.square_ok, st.msd_floor)
+
+
+def adaptive_floor_step(floor: float, msd_seconds: float, total_seconds: float) -> float:
+    """AdaptiveFloor::update's step (client_process_gpu.rs:130-157)."""
+    return lib().nice_adaptive_floor_step(floor, msd_seconds, total_seconds)
+
+
+def adaptive_floor() -> Tuple[float, int]:
+    """The process-wide adaptive MSD floor and its warmup fields left
+    (0xffffffff: pinned by NICE_GPU_MSD_FLOOR)."""
+    f, w = ctypes.c_double(), ctypes.c_uint32()
+    check(lib().nice_adaptive_floor(f, w))
+    return f.value, w.value
 
 
 @dataclass
@@ -235,14 +256,14 @@ class GpuContext:
                 continue
             check(rc)
             lst = [out[i].number_lo | (out[i].number_hi << 64) for i in range(n.value)]
-            stats = NiceonlyStats(st.ranges, st.range_numbers, st.candidates, st.launches,
-                                  st.msd_seconds, st.total_seconds, st.square_ok)
-            return lst, stats
+            return lst, _stats(st)
 
     @staticmethod
     def _nice_opts(msd_floor=0, chunk_size=0, threads=0, stride_k=0, msd_where="auto",
                    deal_stride=0, deal_offset=0):
         where = {"auto": 0, "host": 1, "device": 2}[msd_where]
+        if msd_floor == "adaptive":  # client_process_gpu.rs:96-184
+            msd_floor = _lib.NICE_MSD_FLOOR_ADAPTIVE
         return _lib.nice_niceonly_opts(msd_floor, chunk_size, threads, stride_k, where,
                                        deal_stride, deal_offset, 0)
 
@@ -267,8 +288,7 @@ class GpuContext:
                 continue
             check(rc)
             return ([out[i].number_lo | (out[i].number_hi << 64) for i in range(n.value)],
-                    NiceonlyStats(st.ranges, st.range_numbers, st.candidates, st.launches,
-                                  st.msd_seconds, st.total_seconds, st.square_ok))
+                    _stats(st))
 
     # -- both modes of one field ---------------------------------------------
     def both_raw(self, det_range, nice_range, base: int, **nice_opts):

@@ -36,6 +36,10 @@ from .types import DataToClient, DataToServer, SearchMode
 log = logging.getLogger("nice_client")
 
 
+def _msd_floor(v: str):
+    return v if v == "adaptive" else int(v)
+
+
 def parse_args(argv=None):
     env = os.environ.get
     p = argparse.ArgumentParser(prog="nice_client", description=__doc__.split("\n")[0])
@@ -61,7 +65,10 @@ def parse_args(argv=None):
                    help="explicit field: half-open [START, END)")
     p.add_argument("--hi-base-size", type=int, default=None,
                    help="hi-base field size (code: 1e9, doc/BASELINE: 1e6)")
-    p.add_argument("--msd-floor", type=int, default=0, help="niceonly MSD floor (0 = 250)")
+    p.add_argument("--msd-floor", type=_msd_floor, default=0,
+                   help="niceonly MSD floor: a number (0 = 250, or NICE_GPU_MSD_FLOOR), or "
+                        "'adaptive' for the reference GPU path's adaptive floor "
+                        "(client_process_gpu.rs:96-184)")
     return p.parse_args(argv)
 
 

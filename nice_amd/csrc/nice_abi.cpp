@@ -12,6 +12,7 @@
 // waits for the host between fields (nice_*_submit / nice_*_collect).  The
 // synchronous reference-shaped entry points are submit + collect.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <atomic>
@@ -227,6 +228,7 @@ struct NiceJob {
     nice_niceonly_stats st{};
     std::chrono::steady_clock::time_point t0;
     std::vector<Entry> all;
+    bool adapt = false;            // host-MSD field on the adaptive floor: update it at collect
 };
 
 }  // namespace
@@ -1045,6 +1047,68 @@ static uint64_t env_msd_floor() {
     return v;
 }
 
+// The reference GPU path's AdaptiveFloor (client_process_gpu.rs:96-184),
+// selected by msd_floor = NICE_MSD_FLOOR_ADAPTIVE.  Process-wide, like the
+// reference's OnceLock: NICE_GPU_MSD_FLOOR pins it (no adaptation); otherwise
+// the seed is 512 000 / logical cores clamped to [250, 256 000], the first 3
+// fields do not adapt, and after each host-MSD field the floor moves by
+// msd / gpu_tail, clamped to [1/1.5, 1.5] (nice_adaptive_floor_step).
+namespace {
+constexpr double kFloorMin = 250.0, kFloorMax = 256000.0, kAdaptMaxStep = 1.5, kAdaptMinSecs = 0.002,
+                 kAdaptBaseCoreProduct = 512000.0;
+constexpr uint32_t kAdaptWarmup = 3, kAdaptPinned = 0xffffffffu;
+struct AdaptiveFloor {
+    double floor;
+    uint32_t warmup;  // fields left before adapting; kAdaptPinned: fixed by the environment
+};
+std::mutex g_af_mu;
+
+// std::thread::available_parallelism on Linux: the affinity mask, capped by
+// a cgroup v2 cpu.max quota.
+unsigned available_parallelism() {
+    unsigned n = std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0 && CPU_COUNT(&set) > 0) n = (unsigned)CPU_COUNT(&set);
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        unsigned long period = 0;
+        if (fscanf(f, "%31s %lu", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+            const unsigned long quota = strtoul(q, nullptr, 10);
+            const unsigned c = (unsigned)((quota + period - 1) / period);
+            if (c >= 1 && c < n) n = c;
+        }
+        fclose(f);
+    }
+    return n ? n : 4;
+}
+
+AdaptiveFloor &adaptive_floor() {  // call under g_af_mu
+    static AdaptiveFloor af = [] {
+        if (const uint64_t pin = env_msd_floor()) return AdaptiveFloor{(double)pin, kAdaptPinned};
+        const double seed = std::min(kFloorMax, std::max(kFloorMin, kAdaptBaseCoreProduct / available_parallelism()));
+        return AdaptiveFloor{seed, kAdaptWarmup};
+    }();
+    return af;
+}
+}  // namespace
+
+double nice_adaptive_floor_step(double floor, double msd_seconds, double total_seconds) {
+    const double gpu_tail = std::max(0.0, total_seconds - msd_seconds);
+    const double ratio = gpu_tail < kAdaptMinSecs ? kAdaptMaxStep
+                         : msd_seconds < kAdaptMinSecs ? 1.0 / kAdaptMaxStep
+                                                       : msd_seconds / gpu_tail;
+    const double factor = std::min(kAdaptMaxStep, std::max(1.0 / kAdaptMaxStep, ratio));
+    return std::min(kFloorMax, std::max(kFloorMin, floor * factor));
+}
+
+int nice_adaptive_floor(double *floor, uint32_t *warmup) {
+    std::lock_guard<std::mutex> g(g_af_mu);
+    const AdaptiveFloor &af = adaptive_floor();
+    if (floor) *floor = af.floor;
+    if (warmup) *warmup = af.warmup;
+    return NICE_OK;
+}
+
 int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, uint64_t end_lo,
                          uint64_t end_hi, uint32_t base, const nice_niceonly_opts *opts, int *ticket) {
     using clock = std::chrono::steady_clock;
@@ -1055,8 +1119,14 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
     if (s >= e)
         return fail(NICE_ERR_INVALID, "Range has invalid bounds, range_start must be < range_end");
     nice_niceonly_stats st{};
+    const bool adaptive = opts && opts->msd_floor == NICE_MSD_FLOOR_ADAPTIVE;
     uint64_t floor_size = opts && opts->msd_floor ? opts->msd_floor : env_msd_floor();
+    if (adaptive) {
+        std::lock_guard<std::mutex> g(g_af_mu);
+        floor_size = (uint64_t)adaptive_floor().floor;  // gpu_msd_floor(), client_process_gpu.rs:559-561
+    }
     if (!floor_size) floor_size = 250;
+    st.msd_floor = floor_size;
     const uint32_t k = opts && opts->stride_k ? opts->stride_k : 2;
     int threads = opts && opts->threads > 0 ? opts->threads : (int)std::thread::hardware_concurrency();
     if (threads < 1) threads = 1;
@@ -1303,6 +1373,7 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
     const bool on_device = where == NICE_MSD_DEVICE ||
                            (where == NICE_MSD_AUTO && k == 2 && !((e - s) >> 63) && chunk <= ((u128)1 << 40));
     job.on_device = on_device;
+    job.adapt = adaptive && !on_device;  // the floor balances the host MSD producer against the GPU
     int rc = NICE_OK;
     if (on_device) {
         rc = run_device();
@@ -1492,6 +1563,16 @@ int nice_niceonly_collect(nice_ctx *ctx, int t, nice_number *out, size_t cap, si
         job.st.total_seconds =
             std::chrono::duration<double>(std::chrono::steady_clock::now() - job.t0).count();
         job.collected = true;
+        if (job.adapt) {  // update_msd_floor (client_process_gpu.rs:551, 563-568, 130-157)
+            std::lock_guard<std::mutex> g(g_af_mu);
+            AdaptiveFloor &af = adaptive_floor();
+            if (af.warmup == kAdaptPinned) {
+            } else if (af.warmup > 0) {
+                af.warmup--;
+            } else {
+                af.floor = nice_adaptive_floor_step(af.floor, job.st.msd_seconds, job.st.total_seconds);
+            }
+        }
     }
     if (stats) *stats = job.st;
     const int rc = emit_list(job.all, out, cap, n_out);

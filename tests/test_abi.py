@@ -23,7 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_library_exports_header_symbols():
     with open(os.path.join(ROOT, "include", "nice_hip.h")) as f:
         hdr = f.read()
-    declared = set(re.findall(r"^\s*(?:int|void|const char|uint32_t|uint64_t)\s*\*?\s*(nice_\w+)\(",
+    declared = set(re.findall(r"^\s*(?:int|void|const char|uint32_t|uint64_t|double)\s*\*?\s*(nice_\w+)\(",
                               hdr, re.M))
     assert declared, "no declarations parsed"
     assert declared == set(_lib.EXPORTS)
@@ -310,3 +310,56 @@ def test_fd_bases_and_limb_count_cuts():
         n = ctypes.c_size_t()
         assert L.nice_fd_segment_cuts(base, buf, 8, n) == 0
         assert [buf[2 * i] | (buf[2 * i + 1] << 64) for i in range(n.value)] == want, base
+
+
+def _af_step_ref(floor, msd, total):
+    """AdaptiveFloor::update's step, restated from client_process_gpu.rs:130-157."""
+    gpu_tail = max(total - msd, 0.0)
+    if gpu_tail < 0.002:
+        ratio = 1.5
+    elif msd < 0.002:
+        ratio = 1.0 / 1.5
+    else:
+        ratio = msd / gpu_tail
+    factor = min(max(ratio, 1.0 / 1.5), 1.5)
+    return min(max(floor * factor, 250.0), 256_000.0)
+
+
+def test_adaptive_floor_step_matches_reference_rule():
+    cases = [(32_000, 0.5, 1.0), (32_000, 0.9, 1.0), (32_000, 0.1, 1.0), (300, 0.001, 0.5),
+             (250, 0.0, 0.0), (200_000, 2.0, 2.001), (256_000, 3.0, 4.0), (1000, 0.004, 0.010),
+             (1000, 0.0019, 0.010), (1000, 0.5, 0.5019), (12_345.6, 0.25, 0.75)]
+    rng = random.Random(7)
+    for _ in range(200):
+        m = rng.uniform(0, 2)
+        cases.append((rng.uniform(100, 300_000), m, m + rng.choice([0.0, 0.001, rng.uniform(0, 3)])))
+    for f, m, t in cases:
+        assert N.adaptive_floor_step(f, m, t) == pytest.approx(_af_step_ref(f, m, t), rel=1e-12), (f, m, t)
+
+
+def test_adaptive_floor_seed_and_pin():
+    """The process-wide floor (client_process_gpu.rs:160-184): seeded at
+    512 000 / logical cores clamped to [250, 256 000] with 3 warmup fields,
+    or pinned by NICE_GPU_MSD_FLOOR (no adaptation).  Fresh processes: the
+    state is per process, as the reference's OnceLock."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, os; sys.path.insert(0, %r); import nice_amd as N; f, w = N.adaptive_floor(); "
+            "print(f, w, len(os.sched_getaffinity(0)))" % root)
+
+    def run(env_val):
+        env = dict(os.environ)
+        env.pop("NICE_GPU_MSD_FLOOR", None)
+        if env_val is not None:
+            env["NICE_GPU_MSD_FLOOR"] = env_val
+        out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                             timeout=120, check=True)
+        f, w, cpus = out.stdout.split()
+        return float(f), int(w), int(cpus)
+
+    f, w, cpus = run(None)
+    assert w == 3
+    assert 250 <= f <= 256_000 and f >= min(256_000.0, 512_000.0 / cpus)  # cgroup quota can only lower cores
+    assert run("64000")[:2] == (64000.0, 0xFFFFFFFF)
+    assert run("bogus")[1] == 3

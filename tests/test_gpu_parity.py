@@ -528,10 +528,42 @@ def test_env_msd_floor_pins_the_floor():
     assert run("bogus") == run(None) == ctx_free_candidates(s, s + 10 ** 8, 250)
 
 
-def ctx_free_candidates(a, b, floor):
+def test_adaptive_msd_floor_host_path():
+    """msd_floor="adaptive" (AdaptiveFloor, client_process_gpu.rs:96-184,
+    551-568) on the host-MSD path, in a fresh process: each field's floor is
+    the seed for the 3 warmup fields, then follows the reference's step of the
+    previous field's msd / gpu-tail seconds; the candidates are a superset of
+    the floor-250 set and the nice list is the oracle's."""
+    import subprocess
+    import sys
+    s40 = O.base_range(40)[0]
+    fields = [(47, 100, 10)] + [(s40 + k * 5 * 10 ** 7, s40 + (k + 1) * 5 * 10 ** 7, 40) for k in range(5)]
+    code = ("import sys, json; sys.path.insert(0, %r); import nice_amd as N; c = N.GpuContext(0); "
+            "f0 = N.adaptive_floor(); out = []\n"
+            "for a, b, base in %r:\n"
+            "    lst, st = c.niceonly_raw(a, b, base, msd_floor='adaptive', msd_where='host')\n"
+            "    out.append([lst, st.msd_floor, st.msd_seconds, st.total_seconds, st.candidates])\n"
+            "print(json.dumps([f0, out, N.adaptive_floor()]))" % (ROOT, fields))
+    env = dict(os.environ)
+    env.pop("NICE_GPU_MSD_FLOOR", None)
+    res = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                         timeout=300, check=True)
+    (floor, warm), rows, last = json.loads(res.stdout.strip().splitlines()[-1])
+    assert warm == 3
+    for k, ((a, b, base), (lst, used, msd, total, cands)) in enumerate(zip(fields, rows)):
+        assert used == int(floor), (k, used, floor)
+        if k >= 3:
+            floor = N.adaptive_floor_step(floor, msd, total)
+        want, _ = O.process_range_niceonly(a, b, base)
+        assert lst == [n for n, _ in want.nice_numbers]
+        assert cands >= ctx_free_candidates(a, b, 250, base)
+    assert last[0] == pytest.approx(floor) and last[1] == 0
+
+
+def ctx_free_candidates(a, b, floor, base=40):
     c = N.GpuContext(0)
     try:
-        return c.niceonly_raw(a, b, 40, msd_floor=floor)[1].candidates
+        return c.niceonly_raw(a, b, base, msd_floor=floor)[1].candidates
     finally:
         c.close()
 
