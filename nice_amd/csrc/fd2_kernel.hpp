@@ -42,6 +42,7 @@
 #pragma once
 #include <stdlib.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <type_traits>
@@ -136,7 +137,8 @@ constexpr bool fits64(unsigned base, int digits) {
     return true;
 }
 
-template <int BASE_, int ND_, int NE_, int NE2_, int PROBE_ = 0, int WG_ = 512, int VD_ = 0, int LG_ = -1>
+template <int BASE_, int ND_, int NE_, int NE2_, int PROBE_ = 0, int WG_ = 512, int VD_ = 0, int LG_ = -1,
+          int PERS_ = -1>
 struct Cfg {
     static constexpr int BASE = BASE_;
     // Bottleneck probes (timing experiments only, results are wrong): 1 = no
@@ -249,6 +251,15 @@ struct Cfg {
     // too, and LG 8 removes it (b80 1e9 7.45 -> 7.31 ms, lg_sweep.log).
     // -1: the per-base default.
     static constexpr int LG = LG_ >= 0 ? LG_ : (MW == 3 && WG >= 1024 ? 8 : 0);
+    // Persistent grid: one round of resident workgroups, each walking a
+    // contiguous range of 64-unit batches that its waves pull from an LDS
+    // counter as they finish (instead of one chunk per lane and many rounds
+    // of workgroups, where a workgroup's CU idles down while its slowest
+    // wave finishes: b54 1e9, one 1024-thread workgroup per CU, waited 61 us
+    // of a 134 us workgroup life for it, profiles/r03/fd2_stamps_b54.log).
+    // -1: the per-base default.
+    static constexpr bool PERS = PERS_ >= 0 ? PERS_ != 0 : false;
+    static_assert(!(PERS && SPLIT), "persistent lanes count more than a u8 counter holds");
     // VD & 256 (no low-digit table only): limb 0 of S and of C by VALU too --
     // n^2 mod B and n^3 mod B of a wave's lanes keep few residues mod 16, so
     // their lookups pile onto few bank quads
@@ -769,6 +780,7 @@ struct Fd2Args {
     u32 tail_count, main_blocks;
     u32 cutoff;
     u32 ncopies;        // histogram copies in use (<= kHistCopies), the same for every launch of a field
+    u32 wave_cap;       // persistent grid: batches one wave may take (its lanes' u16 counters hold them)
     u64 *hist;          // kHistCopies x 129 bins
     NumOut out;
     const uint4 *tabs;
@@ -834,6 +846,95 @@ __device__ __forceinline__ void field_finish(const FieldFinish &fin, u64 *hist, 
         __hip_atomic_store(&fin.out_mapped[130], fin.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// One lane's chunk: `chunk` numbers from n0 (the state at n0 built by init;
+// the cached high limbs' mask is built here, it needs the tables).
+template <class P>
+__device__ __forceinline__ void walk_chunk(State<P> &st, const unsigned char *smem, u32 chunk, u64 n0_lo,
+                                           u64 n0_hi, u32 hbase, u32 hinc, u32 *outl, u32 cutoff,
+                                           const NumOut &out, u32 &probe_acc) {
+    recompute_hi<P>(st, smem);
+    const u32 r80 = st.r8;
+    for (u32 i = 0; i < chunk; i++) {
+        u32 m[P::MW], w1 = 0;
+#pragma unroll
+        for (int w = 0; w < P::MW; w++) m[w] = st.hi[w];
+        if constexpr (P::PROBE & 1) {
+            m[0] |= st.r8;
+            w1 = st.r8 & 0xff;
+#pragma unroll
+            for (int q = P::LO; q < P::SL; q++) m[q & 1] |= st.S[q];
+#pragma unroll
+            for (int q = P::LO; q < P::CL; q++) m[q & 1] |= st.C[q];
+        } else {
+            if constexpr (P::LSD) {
+                const uint2 v = *(const uint2 *)(smem + P::TL + st.r8);
+                m[0] |= v.x;
+                m[1] |= v.y & P::DMASK;
+                w1 = v.y;
+            }
+#pragma unroll
+            for (int q = P::LO; q < P::SL; q++) {
+                if ((P::PROBE & 4) && q == 1) { m[0] |= st.S[q] & 0xffu; continue; }  // probe: no limb-1 lookups
+                if (q >= P::SL - P::VDS || (P::VDL && q == 0)) or_valu<P>(st.S[q] - P::EBT, m);
+                else or_entry<P>(smem + (P::TB - P::EBT) + st.S[q], m);
+                if (P::LG && (q - P::LO + 1) % P::LG == 0) lookup_group_end<P>(m);
+            }
+#pragma unroll
+            for (int q = P::LO; q < P::CL; q++) {
+                if ((P::PROBE & 4) && q == 1) { m[1] |= st.C[q] & 0xffu; continue; }
+                if (q >= P::CL - P::VDC || (P::VDL && q == 0)) or_valu<P>(st.C[q], m);
+                else or_entry<P>(smem + P::TB + st.C[q], m);
+                if (P::LG && (P::SL + q - 2 * P::LO + 1) % P::LG == 0) lookup_group_end<P>(m);
+            }
+        }
+        // uw = unique count - W0: the bias rides in the first v_bcnt's
+        // accumulator operand (an SGPR; LLVM would add it separately).
+        u32 uw = bcnt_acc(m[0], (u32)(-P::W0));
+#pragma unroll
+        for (int w = 1; w < P::MW; w++) uw += __popc(m[w]);
+        if (uw < (u32)P::W) {
+            if constexpr (P::PROBE & 2) probe_acc++;
+            else atomicAdd((u32 *)(smem + uw * (P::HROW * 4) + hbase), hinc);
+        } else {
+            const u32 u = uw + P::W0;
+            atomicAdd(&outl[u], 1u);
+            if (u > cutoff) {
+                u64 lo = n0_lo, hi = n0_hi;
+                add_u128(lo, hi, (st.r8 - r80) / P::ES);  // = i (keeps i scalar)
+                u32 pos = atomicAdd(out.count, 1u);
+                if (pos < out.cap) {
+                    out.n[2 * (u64)pos] = lo;
+                    out.n[2 * (u64)pos + 1] = hi;
+                    out.u[pos] = u;
+                }
+            }
+        }
+        step<P>(st, smem, w1);
+    }
+}
+
+// Persistent grid: batch b of the launch (64 lanes' units) -> this lane's
+// unit: b < mb: main unit 64 b + lane (chunk a.chunk from a.start); else the
+// tail numbers 64 (b - mb) + lane (chunk 1 from a.tail).
+__device__ __forceinline__ void pers_unit(const Fd2Args &a, u32 b, u32 mb, u32 lane, bool &active, u64 &lo,
+                                          u64 &hi, u32 &chunk) {
+    if (b < mb) {
+        const u32 unit = 64 * b + lane;
+        active = unit < a.nunits;
+        lo = a.start_lo;
+        hi = a.start_hi;
+        add_u128(lo, hi, (u64)unit * a.chunk);
+        chunk = a.chunk;
+    } else {
+        const u32 idx = 64 * (b - mb) + lane;
+        active = idx < a.tail_count;
+        lo = a.tail_lo;
+        hi = a.tail_hi;
+        add_u128(lo, hi, (u64)idx);
+        chunk = 1;
+    }
+}
+
 template <class P>
 __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
     // Static LDS: its address is a compile-time constant, so a lookup is one
@@ -875,13 +976,32 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
             for (u32 i = tid; i < (u32)(P::HIST_BYTES / 16); i += P::WG)
                 h4[P::HB / 16 + i] = make_uint4(0, 0, 0, 0);
     }
-    // A lane takes at most ONE chunk (launch_cfg sizes the grid to cover every
-    // unit), so its state is built while the table DMA is in flight; only the
-    // cached high limbs' mask needs the tables.
-    const u32 unit = blk * P::WG + tid;
-    const bool active = unit < nunits;
+    // A lane's first chunk (without PERS its only one: launch_cfg sizes the
+    // grid to cover every unit) is set up while the table DMA is in flight;
+    // only the cached high limbs' mask needs the tables.
+    const u32 lane_id = tid & 63;
+    u32 unit = blk * P::WG + tid;
+    bool active = unit < nunits;
     u64 n0_lo = start_lo, n0_hi = start_hi;
-    add_u128(n0_lo, n0_hi, (u64)unit * chunk);
+    u32 chunk_l = chunk;
+    // persistent grid: this workgroup's batches are b = blockIdx + G k, k <
+    // pnk, of the launch's nb = mb main + tail batches (strided, so every
+    // workgroup samples the whole field: contiguous slabs were up to 40 %
+    // slower on some n-ranges, profiles/r03/fd2_stamps_pers.log), and the
+    // next k to hand out
+    __shared__ u32 pers_next;
+    u32 pmb = 0, pnk = 0, pk = 0;
+    if constexpr (P::PERS) {
+        pmb = (a.nunits + 63) / 64;
+        const u32 nb = pmb + (a.tail_count + 63) / 64, G = gridDim.x;
+        pnk = nb > blockIdx.x ? (nb - blockIdx.x + G - 1) / G : 0;
+        pk = tid >> 6;
+        if (tid == 0) pers_next = P::WG / 64;
+        if (pk < pnk) pers_unit(a, blockIdx.x + G * pk, pmb, lane_id, active, n0_lo, n0_hi, chunk_l);
+        else active = false;
+    } else {
+        add_u128(n0_lo, n0_hi, (u64)unit * chunk);
+    }
     State<P> st;
     if (active) init<P>(st, n0_lo, n0_hi);
     __syncthreads();  // drains the DMA (vmcnt(0)) before the barrier
@@ -891,66 +1011,31 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
     const u32 hbase = P::HB + tid % P::HROW * 4;
     const u32 hinc = 1u << (32 / P::HQ * (tid / P::HROW));
     u32 probe_acc = 0;
-    if (active) {
-        recompute_hi<P>(st, smem);
-        FD2_STAMP(a, 2);  // thread 0's cached mask done
-        const u32 r80 = st.r8;
-        for (u32 i = 0; i < chunk; i++) {
-            u32 m[P::MW], w1 = 0;
-#pragma unroll
-            for (int w = 0; w < P::MW; w++) m[w] = st.hi[w];
-            if constexpr (P::PROBE & 1) {
-                m[0] |= st.r8;
-                w1 = st.r8 & 0xff;
-#pragma unroll
-                for (int q = P::LO; q < P::SL; q++) m[q & 1] |= st.S[q];
-#pragma unroll
-                for (int q = P::LO; q < P::CL; q++) m[q & 1] |= st.C[q];
-            } else {
-                if constexpr (P::LSD) {
-                    const uint2 v = *(const uint2 *)(smem + P::TL + st.r8);
-                    m[0] |= v.x;
-                    m[1] |= v.y & P::DMASK;
-                    w1 = v.y;
-                }
-#pragma unroll
-                for (int q = P::LO; q < P::SL; q++) {
-                    if ((P::PROBE & 4) && q == 1) { m[0] |= st.S[q] & 0xffu; continue; }  // probe: no limb-1 lookups
-                    if (q >= P::SL - P::VDS || (P::VDL && q == 0)) or_valu<P>(st.S[q] - P::EBT, m);
-                    else or_entry<P>(smem + (P::TB - P::EBT) + st.S[q], m);
-                    if (P::LG && (q - P::LO + 1) % P::LG == 0) lookup_group_end<P>(m);
-                }
-#pragma unroll
-                for (int q = P::LO; q < P::CL; q++) {
-                    if ((P::PROBE & 4) && q == 1) { m[1] |= st.C[q] & 0xffu; continue; }
-                    if (q >= P::CL - P::VDC || (P::VDL && q == 0)) or_valu<P>(st.C[q], m);
-                    else or_entry<P>(smem + P::TB + st.C[q], m);
-                    if (P::LG && (P::SL + q - 2 * P::LO + 1) % P::LG == 0) lookup_group_end<P>(m);
-                }
+    FD2_STAMP(a, 2);  // (the cached mask is built inside walk_chunk)
+    if constexpr (!P::PERS) {
+        if (active) {
+            walk_chunk<P>(st, smem, chunk, n0_lo, n0_hi, hbase, hinc, outl, cutoff, out, probe_acc);
+        }
+    } else {
+        // Persistent grid: wave w starts on this workgroup's batch k = w (its
+        // state is already built), then pulls the next k from the LDS counter
+        // until the workgroup's batches are exhausted or the wave has taken
+        // wave_cap of them (its lanes' u16 counters hold them; the host sizes
+        // launches so the waves' caps cover the workgroup's batches).
+        u32 k = pk, taken = 0;
+        bool act = active;
+        u64 m_lo = n0_lo, m_hi = n0_hi;
+        u32 ch = chunk_l;
+        while (k < pnk) {
+            if (taken) {
+                pers_unit(a, blockIdx.x + gridDim.x * k, pmb, lane_id, act, m_lo, m_hi, ch);
+                if (act) init<P>(st, m_lo, m_hi);
             }
-            // uw = unique count - W0: the bias rides in the first v_bcnt's
-            // accumulator operand (an SGPR; LLVM would add it separately).
-            u32 uw = bcnt_acc(m[0], (u32)(-P::W0));
-#pragma unroll
-            for (int w = 1; w < P::MW; w++) uw += __popc(m[w]);
-            if (uw < (u32)P::W) {
-                if constexpr (P::PROBE & 2) probe_acc++;
-                else atomicAdd((u32 *)(smem + uw * (P::HROW * 4) + hbase), hinc);
-            } else {
-                const u32 u = uw + P::W0;
-                atomicAdd(&outl[u], 1u);
-                if (u > cutoff) {
-                    u64 lo = n0_lo, hi = n0_hi;
-                    add_u128(lo, hi, (st.r8 - r80) / P::ES);  // = i (keeps i scalar)
-                    u32 pos = atomicAdd(out.count, 1u);
-                    if (pos < out.cap) {
-                        out.n[2 * (u64)pos] = lo;
-                        out.n[2 * (u64)pos + 1] = hi;
-                        out.u[pos] = u;
-                    }
-                }
-            }
-            step<P>(st, smem, w1);
+            if (act) walk_chunk<P>(st, smem, ch, m_lo, m_hi, hbase, hinc, outl, cutoff, out, probe_acc);
+            if (++taken >= a.wave_cap) break;
+            u32 nk = 0;
+            if (lane_id == 0) nk = atomicAdd(&pers_next, 1u);
+            k = __builtin_amdgcn_readfirstlane(__shfl(nk, 0));
         }
     }
     if constexpr ((P::PROBE & 2) != 0) atomicAdd(&outl[P::W0], probe_acc);  // mass only
@@ -1086,6 +1171,7 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         a.main_blocks = (u32)main_blocks;
         a.cutoff = q.cutoff;
         a.ncopies = q.hist_copies;
+        a.wave_cap = (u32)(65535 / chunk);
         a.hist = q.hist;
         a.out = q.out;
         a.tabs = tabs;
@@ -1093,11 +1179,24 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         a.fin = left == cnt ? q.fin : FieldFinish{nullptr, nullptr};
 #ifdef NICE_PROBES
         {
-            const u64 v[6] = {main_blocks + tail_blocks, (u64)P::WG, chunk, nunits, tail, (u64)per_cu};
+            const u64 v[6] = {P::PERS ? std::min<u64>((u64)num_cus * per_cu, ((nunits + 63) / 64 + (tail + 63) / 64 +
+                                                                            P::WG / 64 - 1) / (P::WG / 64))
+                                      : main_blocks + tail_blocks,
+                              (u64)P::WG, chunk, nunits, tail, (u64)per_cu};
             for (int k = 0; k < 6; k++) g_last_launch[k] = v[k];
         }
 #endif
-        hipLaunchKernelGGL(kern, dim3((u32)(main_blocks + tail_blocks)), dim3(P::WG), 0, s, a);
+        u64 grid = main_blocks + tail_blocks;
+        if constexpr (P::PERS) {
+            // one round of resident workgroups (fewer when the batches run out);
+            // a.nunits < 2^32 - 63 keeps the batch count in 32 bits
+            const u64 nb = (nunits + 63) / 64 + (tail + 63) / 64, nw = P::WG / 64;
+            grid = std::min<u64>((u64)num_cus * per_cu, (nb + nw - 1) / nw);
+            if (nunits > 0xffffffc0ull) return hipErrorInvalidValue;
+            // every workgroup's range fits its waves' caps (u16 counters)
+            if ((nb + grid - 1) / grid > nw * a.wave_cap) return hipErrorInvalidValue;
+        }
+        hipLaunchKernelGGL(kern, dim3((u32)grid), dim3(P::WG), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         add_u128(q.start_lo, q.start_hi, cnt);
         left -= cnt;

@@ -41,6 +41,16 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
         case 358: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 258>>(p, num_cus, s);
         default: break;
         }
+        // Persistent grid A/B (NICE_FD2_PERS = 1: on, 2: off)
+        switch ((int)probe_knob("NICE_FD2_PERS", 0)) {
+        case 1:
+            return wg512 ? launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, valu_limbs(B_), -1, 1>>(p, num_cus, s)
+                         : launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), valu_limbs(B_), -1, 1>>(p, num_cus, s);
+        case 2:
+            return wg512 ? launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, valu_limbs(B_), -1, 0>>(p, num_cus, s)
+                         : launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), valu_limbs(B_), -1, 0>>(p, num_cus, s);
+        default: break;
+        }
         // Lookup-group sweep of the three-mask-word bases (NICE_FD2_LG = LG,
         // or 1000 + LG: the split b64 + u16 layout with that grouping)
         if constexpr ((B_ + 31) / 32 == 3) {
