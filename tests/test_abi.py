@@ -264,19 +264,22 @@ def test_product_library_has_no_probe_kernels():
     import subprocess
     syms = subprocess.run(["nm", "-C", _lib.LIB_PATH], capture_output=True, text=True,
                           check=True).stdout
-    cfgs = re.findall(r"fd2_kernel<nice::fd2::Cfg<(\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (-?\d+)>",
-                      syms)
+    cfgs = [[int(x) for x in m.split(", ")]
+            for m in re.findall(r"fd2_kernel<nice::fd2::Cfg<(-?\d+(?:, -?\d+)*)>", syms)]
     assert cfgs, "no fd2 kernels found"
-    assert all(c[4] == "0" for c in cfgs), "probe instantiation in the product library"
+    # Cfg<BASE, ND, NE, NE2, PROBE, WG, VD, LG, PERS>
+    assert all(len(c) == 9 for c in cfgs), cfgs[:3]
+    assert all(c[4] == 0 for c in cfgs), "probe instantiation in the product library"
     # neither the split b64 + u16 table layout (VD & 512) nor a forced lookup
-    # grouping (LG >= 0: the per-base default is -1) is a product variant
-    assert all(int(c[6]) & 512 == 0 and c[7] == "-1" for c in cfgs), "probe layout in the product library"
+    # grouping or persistence (the per-base defaults are -1) is a product variant
+    assert all(c[6] & 512 == 0 and c[7] == -1 and c[8] == -1 for c in cfgs), \
+        "probe variant in the product library"
     assert "detailed_fd_kernel" not in syms
     with open(_lib.LIB_PATH, "rb") as f:
         blob = f.read()
     for knob in (b"NICE_FD2_PROBE", b"NICE_MSD_PROBE", b"NICE_FD_VARIANT", b"NICE_FD2_TCHUNK",
                  b"NICE_FD2_MINCHUNK", b"NICE_FD2_WG512", b"NICE_MSD_TRACE", b"NICE_FD2_LG",
-                 b"NICE_FD2_COPIES", b"NICE_FD2_VD"):
+                 b"NICE_FD2_COPIES", b"NICE_FD2_VD", b"NICE_FD2_PERS"):
         assert knob not in blob, knob
 
 
