@@ -137,6 +137,42 @@ constexpr bool fits64(unsigned base, int digits) {
     return true;
 }
 
+// LDS bytes / waves per SIMD of a base's kernel at a workgroup size (the
+// formulas of Cfg, evaluated without instantiating it).
+constexpr int lds_bytes(int base, int wg) {
+    const int mw = (base + 31) / 32, es = mw == 1 ? 4 : (mw == 2 ? 8 : 16), b2 = base * base;
+    int t = 0;
+    while ((1 << t) < b2) t++;
+    const int ebt = es * ((1 << t) - b2);
+    const int tb0 = (window_w(base) * (wg / 2) * 4 + 4 * (base + 1) + 15) / 16 * 16;
+    const int tb = tb0 >= ebt ? tb0 : (ebt + 15) / 16 * 16;
+    const int db = base - 32;
+    const bool lsd = mw == 2 && db > 0 && db + (db > 20 ? 4 : 10) <= 30;
+    return tb + (b2 * es + 15) / 16 * 16 + (lsd ? (2 * b2 * es + 15) / 16 * 16 : 0);
+}
+// Waves per SIMD actually resident: the LDS and VGPR caps, in whole
+// workgroups (a workgroup puts wg / 256 waves on each SIMD).
+constexpr int waves_at(int base, int wg) {
+    const int lds = (163840 / lds_bytes(base, wg)) * (wg / 64) / 4;
+    const int cap = lds < state_waves(base) ? lds : state_waves(base);
+    return cap / (wg / 256) * (wg / 256);
+}
+// Workgroup size for fields >= 1e7: the kernels are bound by LDS lookups and
+// want as many in flight as fit, so the size with more waves per SIMD under
+// the LDS budget wins, 512 on a tie.  Measured on the first three bases: b40
+// two 1024-thread workgroups per CU (8 waves/SIMD) 2.38 ms vs 2.43 for three
+// 512-thread ones (6 waves, profiles/r01/fd2_wg_sweep2.log); b80 one
+// 1024-thread workgroup (4 waves) 8.47 ms vs 9.37 at 512 (2 waves,
+// profiles/r01/b80_wg_sweep.log); b50 4 waves either way, 512 kept.
+constexpr int big_wg(int base) { return waves_at(base, 1024) > waves_at(base, 512) ? 1024 : 512; }
+
+// Persistent grid by default where the kernel holds ONE workgroup per CU
+// (b52..58, b65..68, b80 at 1024 threads): with two or more, a workgroup's
+// draining tail overlaps another's steps, and rounds of workgroups win
+// (profiles/r03/pers_sweep_all.log: b52..58 -12..-15 %, b65..68 / b80 -6..-10 %
+// per 1e9; b42..50 and b59..64, two workgroups per CU, +1..+6 %).
+constexpr bool one_wg_per_cu(int base, int wg) { return waves_at(base, wg) == wg / 256; }
+
 template <int BASE_, int ND_, int NE_, int NE2_, int PROBE_ = 0, int WG_ = 512, int VD_ = 0, int LG_ = -1,
           int PERS_ = -1>
 struct Cfg {
@@ -258,7 +294,10 @@ struct Cfg {
     // wave finishes: b54 1e9, one 1024-thread workgroup per CU, waited 61 us
     // of a 134 us workgroup life for it, profiles/r03/fd2_stamps_b54.log).
     // -1: the per-base default.
-    static constexpr bool PERS = PERS_ >= 0 ? PERS_ != 0 : false;
+    static constexpr bool PERS = PERS_ >= 0 ? PERS_ != 0 : (WG >= 1024 && !SPLIT && one_wg_per_cu(BASE, WG));
+    // the same kernel with rounds of workgroups (launch_cfg falls back to it
+    // when the runtime occupancy or the field size does not suit PERS)
+    using NoPers = Cfg<BASE_, ND_, NE_, NE2_, PROBE_, WG_, VD_, LG_, 0>;
     static_assert(!(PERS && SPLIT), "persistent lanes count more than a u8 counter holds");
     // VD & 256 (no low-digit table only): limb 0 of S and of C by VALU too --
     // n^2 mod B and n^3 mod B of a wave's lanes keep few residues mod 16, so
@@ -1117,13 +1156,19 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
     // Target numbers per lane.  Short chunks put a wave's 64 lanes on nearby n,
     // so the top stepped limbs (and the cached ones) of neighbouring lanes are
     // equal or close and their lookups stop conflicting; a chunk still pays
-    // one init (radix-B conversion and products, ~10 steps).  Each lane takes
-    // one chunk and the grid is many rounds of workgroups, not a persistent
-    // grid: workgroups at different phases (table build, init, steps) share a
-    // CU.  b40 1e9: 2.49 ms persistent at chunk 637, 2.31 persistent at ~80,
-    // 2.19-2.21 at 60-120 non-persistent (scripts/gridx_probe.sh,
-    // profiles/r01/fd2_chunk_sweep.log).
+    // one init (radix-B conversion and products, ~10 steps).  Without PERS
+    // each lane takes one chunk and the grid is many rounds of workgroups:
+    // with two or more workgroups per CU, workgroups at different phases
+    // (table DMA, init, steps, draining) share a CU (b40 1e9 round 1: 2.49 ms
+    // persistent with static lane assignment at chunk 637, 2.31 at ~80,
+    // 2.19-2.21 in rounds, profiles/r01/fd2_chunk_sweep.log).
     const u64 tchunk = probe_knob("NICE_FD2_TCHUNK", (u64)P::TCHUNK);
+    if constexpr (P::PERS) {
+        // The persistent grid pays off where ONE workgroup fills a CU and the
+        // segment needs at least two rounds of them; otherwise (a device with
+        // other occupancy, short segments) the same kernel in rounds.
+        if (per_cu_q != 1 || p.count < 2 * tchunk * lanes) return launch_cfg<typename P::NoPers>(p, num_cus, s);
+    }
     const uint4 *tabs = nullptr;
     if ((e = fd2_tables<P>(s, &tabs)) != hipSuccess) return e;
     DetailedLaunch q = p;
@@ -1210,35 +1255,6 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
 
 namespace nice {
 namespace fd2 {
-
-// LDS bytes / waves per SIMD of a base's kernel at a workgroup size (the
-// formulas of Cfg, evaluated without instantiating it).
-constexpr int lds_bytes(int base, int wg) {
-    const int mw = (base + 31) / 32, es = mw == 1 ? 4 : (mw == 2 ? 8 : 16), b2 = base * base;
-    int t = 0;
-    while ((1 << t) < b2) t++;
-    const int ebt = es * ((1 << t) - b2);
-    const int tb0 = (window_w(base) * (wg / 2) * 4 + 4 * (base + 1) + 15) / 16 * 16;
-    const int tb = tb0 >= ebt ? tb0 : (ebt + 15) / 16 * 16;
-    const int db = base - 32;
-    const bool lsd = mw == 2 && db > 0 && db + (db > 20 ? 4 : 10) <= 30;
-    return tb + (b2 * es + 15) / 16 * 16 + (lsd ? (2 * b2 * es + 15) / 16 * 16 : 0);
-}
-// Waves per SIMD actually resident: the LDS and VGPR caps, in whole
-// workgroups (a workgroup puts wg / 256 waves on each SIMD).
-constexpr int waves_at(int base, int wg) {
-    const int lds = (163840 / lds_bytes(base, wg)) * (wg / 64) / 4;
-    const int cap = lds < state_waves(base) ? lds : state_waves(base);
-    return cap / (wg / 256) * (wg / 256);
-}
-// Workgroup size for fields >= 1e7: the kernels are bound by LDS lookups and
-// want as many in flight as fit, so the size with more waves per SIMD under
-// the LDS budget wins, 512 on a tie.  Measured on the first three bases: b40
-// two 1024-thread workgroups per CU (8 waves/SIMD) 2.38 ms vs 2.43 for three
-// 512-thread ones (6 waves, profiles/r01/fd2_wg_sweep2.log); b80 one
-// 1024-thread workgroup (4 waves) 8.47 ms vs 9.37 at 512 (2 waves,
-// profiles/r01/b80_wg_sweep.log); b50 4 waves either way, 512 kept.
-constexpr int big_wg(int base) { return waves_at(base, 1024) > waves_at(base, 512) ? 1024 : 512; }
 
 // Limbs decoded by VALU instead of a table lookup (Cfg::VD: top C limbs +
 // 16 x top S limbs), per base where the lookups' bank conflicts outweigh the

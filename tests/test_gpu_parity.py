@@ -440,6 +440,26 @@ def test_big_field_kernel_equals_small_field_kernel(ctx, base):
     assert all(O.num_unique_digits(n, base) == u for n, u in l)
 
 
+@pytest.mark.parametrize("base", [55, 58, 65, 67, 68])
+def test_persistent_grid_equals_rounds(ctx, base):
+    """Bases whose big-field kernel holds one workgroup per CU run fields of
+    >= 2 rounds on the persistent grid (waves pull strided 64-unit batches);
+    1e8 windows (< 2 rounds) run in rounds of workgroups.  A 1e9 field must
+    equal the sum of its ten 1e8 windows, and every near-miss recomputes by
+    the oracle.  (b52-54 and b80 1e9 are pinned to oracle fixtures in
+    test_fd_bases_whole_fields_1e9.)"""
+    r0, r1 = O.base_range(base)
+    s = r0 + (r1 - r0) // 3
+    h, l = ctx.detailed_raw(s, s + 10 ** 9, base)
+    hs, ls = [0] * len(h), []
+    for k in range(10):
+        hk, lk = ctx.detailed_raw(s + k * 10 ** 8, s + (k + 1) * 10 ** 8, base)
+        hs = [x + y for x, y in zip(hs, hk)]
+        ls += lk
+    assert h == hs and l == ls and sum(h) == 10 ** 9
+    assert all(O.num_unique_digits(n, base) == u for n, u in l)
+
+
 def test_multi_device_context_sharding():
     import torch
     n = torch.cuda.device_count()
