@@ -157,14 +157,20 @@ constexpr int waves_at(int base, int wg) {
     const int cap = lds < state_waves(base) ? lds : state_waves(base);
     return cap / (wg / 256) * (wg / 256);
 }
-// Workgroup size for fields >= 1e7: the kernels are bound by LDS lookups and
-// want as many in flight as fit, so the size with more waves per SIMD under
-// the LDS budget wins, 512 on a tie.  Measured on the first three bases: b40
-// two 1024-thread workgroups per CU (8 waves/SIMD) 2.38 ms vs 2.43 for three
-// 512-thread ones (6 waves, profiles/r01/fd2_wg_sweep2.log); b80 one
-// 1024-thread workgroup (4 waves) 8.47 ms vs 9.37 at 512 (2 waves,
-// profiles/r01/b80_wg_sweep.log); b50 4 waves either way, 512 kept.
-constexpr int big_wg(int base) { return waves_at(base, 1024) > waves_at(base, 512) ? 1024 : 512; }
+// Workgroup size for fields >= 1e7 in rounds of workgroups: the kernels are
+// bound by LDS lookups and want as many in flight as fit, so the size with
+// more waves per SIMD under the LDS budget wins, 512 on a tie.  Measured on
+// the first three bases: b40 two 1024-thread workgroups per CU (8 waves/SIMD)
+// 2.38 ms vs 2.43 for three 512-thread ones (6 waves,
+// profiles/r01/fd2_wg_sweep2.log); b80 one 1024-thread workgroup (4 waves)
+// 8.47 ms vs 9.37 at 512 (2 waves, profiles/r01/b80_wg_sweep.log); b50 4
+// waves either way, 512 kept.
+constexpr int rounds_wg(int base) { return waves_at(base, 1024) > waves_at(base, 512) ? 1024 : 512; }
+// With the persistent grid (Cfg::PERS) a tie goes to 1024: one 1024-thread
+// workgroup per CU walking strided batches beats two 512-thread ones in
+// rounds on every such base (b42..50 -3..-10 %, b59..64 -2..-5 % per 1e9,
+// profiles/r03/pers_sweep_wg1024.log).
+constexpr int big_wg(int base) { return waves_at(base, 1024) >= waves_at(base, 512) ? 1024 : 512; }
 
 // Persistent grid by default where the kernel holds ONE workgroup per CU
 // (b52..58, b65..68, b80 at 1024 threads): with two or more, a workgroup's
@@ -296,8 +302,9 @@ struct Cfg {
     // -1: the per-base default.
     static constexpr bool PERS = PERS_ >= 0 ? PERS_ != 0 : (WG >= 1024 && !SPLIT && one_wg_per_cu(BASE, WG));
     // the same kernel with rounds of workgroups (launch_cfg falls back to it
-    // when the runtime occupancy or the field size does not suit PERS)
-    using NoPers = Cfg<BASE_, ND_, NE_, NE2_, PROBE_, WG_, VD_, LG_, 0>;
+    // when the runtime occupancy or the field size does not suit PERS), at
+    // the workgroup size rounds prefer
+    using NoPers = Cfg<BASE_, ND_, NE_, NE2_, PROBE_, (PERS_ < 0 ? rounds_wg(BASE_) : WG_), VD_, LG_, 0>;
     static_assert(!(PERS && SPLIT), "persistent lanes count more than a u8 counter holds");
     // VD & 256 (no low-digit table only): limb 0 of S and of C by VALU too --
     // n^2 mod B and n^3 mod B of a wave's lanes keep few residues mod 16, so

@@ -41,7 +41,15 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
         case 358: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 258>>(p, num_cus, s);
         default: break;
         }
-        // Persistent grid A/B (NICE_FD2_PERS = 1: on, 2: off)
+        // Persistent grid A/B (NICE_FD2_PERS = 1: on, 2: off; 3 / 4: 1024-thread
+        // workgroups with / without it, where the LDS and VGPRs allow one)
+        if constexpr (waves_at(B_, 1024) >= 4) {
+            switch ((int)probe_knob("NICE_FD2_PERS", 0)) {
+            case 3: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 1024, valu_limbs(B_), -1, 1>>(p, num_cus, s);
+            case 4: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 1024, valu_limbs(B_), -1, 0>>(p, num_cus, s);
+            default: break;
+            }
+        }
         switch ((int)probe_knob("NICE_FD2_PERS", 0)) {
         case 1:
             return wg512 ? launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, valu_limbs(B_), -1, 1>>(p, num_cus, s)

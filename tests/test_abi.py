@@ -271,8 +271,9 @@ def test_product_library_has_no_probe_kernels():
     assert all(len(c) == 9 for c in cfgs), cfgs[:3]
     assert all(c[4] == 0 for c in cfgs), "probe instantiation in the product library"
     # neither the split b64 + u16 table layout (VD & 512) nor a forced lookup
-    # grouping or persistence (the per-base defaults are -1) is a product variant
-    assert all(c[6] & 512 == 0 and c[7] == -1 and c[8] == -1 for c in cfgs), \
+    # grouping (the per-base default is -1) is a product variant; PERS is the
+    # per-base default (-1) or the rounds fallback of a persistent kernel (0)
+    assert all(c[6] & 512 == 0 and c[7] == -1 and c[8] in (-1, 0) for c in cfgs), \
         "probe variant in the product library"
     assert "detailed_fd_kernel" not in syms
     with open(_lib.LIB_PATH, "rb") as f:
