@@ -1271,11 +1271,13 @@ namespace fd2 {
 // profiles/r02/vd_sweep_low.log).  b64: 6.31 -> 4.25 ms (its table index
 // n^2 mod 4096 keeps few residues mod 32, so lookups pile onto few banks);
 // b45 2.60 -> 2.41; b60 3.79 -> 3.41; b63 3.96 -> 3.70; b68 7.42 -> 6.87;
-// b80 8.22 -> 7.46; b40 neutral (r01).
+// b80 8.22 -> 7.46; b40 neutral (r01).  Re-swept on the persistent grid
+// (profiles/r03/vd_sweep_persistent.log): b55 0 -> 1 (2.91 -> 2.87 ms), b58
+// 1 -> 2 (3.08 -> 3.00); every other base within ~1 % of its choice.
 constexpr int valu_limbs(int base) {
     switch (base) {
-    case 43: case 44: case 45: case 48: case 50: case 54: case 58: return 1;
-    case 53: case 63: case 65: return 2;
+    case 43: case 44: case 45: case 48: case 50: case 54: case 55: return 1;
+    case 53: case 58: case 63: case 65: return 2;
     case 60: case 62: case 67: case 68: case 80: return 256;  // limb 0 by VALU
     case 64: return 258;
     default: return 0;
