@@ -40,13 +40,20 @@ import os
 import sys
 import time
 
-# Hardware queues per process: HIP's default (4, what the GPU box exports and
-# what a Rust client linking libnice_hip.so gets) unless --hw-queues N asks for
-# another value (A/B runs).  Set before HIP initialises; the value used and the
-# exported one are recorded in the JSON line's config.
+# Hardware queues per process: at N = 1 HIP's default (4, what the GPU box
+# exports and what a Rust client linking libnice_hip.so gets).  Under torchrun
+# the process also holds torch's stream and RCCL's next to the library's six
+# slot streams, and on 4 queues the exchange's copies and collective wait
+# behind queued field kernels: a 1/8 shard's step is 0.281 ms at 4 queues,
+# 0.264 at 8, 0.263 at 16 (plain process: 0.259; profiles/r03/dist_hw_queues.log),
+# so the distributed driver asks for 8.  --hw-queues N overrides (A/B runs).
+# Set before HIP initialises; the value used and the exported one are recorded
+# in the JSON line's config.
 HW_QUEUES_EXPORTED = os.environ.get("GPU_MAX_HW_QUEUES")
 if "--hw-queues" in sys.argv:
     os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[sys.argv.index("--hw-queues") + 1]
+elif "WORLD_SIZE" in os.environ:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -85,7 +92,8 @@ def parse():
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                    help="N > 1: RCCL over xGMI (nccl, default) or gloo on host tensors (tests)")
     p.add_argument("--hw-queues", type=int, default=None,
-                   help="GPU_MAX_HW_QUEUES for this process (default: as exported, HIP default 4)")
+                   help="GPU_MAX_HW_QUEUES for this process (default: HIP's 4 at N = 1, 8 under "
+                        "torchrun)")
     p.add_argument("--sync", action="store_true",
                    help="synchronous library calls (no cross-field pipelining)")
     return p.parse_args()

@@ -36,9 +36,15 @@
 //    above the window) take a divergent branch to a per-workgroup LDS
 //    histogram and the global near-miss list.  One flush per workgroup.
 //
+//  * Grid: rounds of workgroups, one chunk per lane, where two or more
+//    workgroups share a CU (b40); one round of resident 1024-thread
+//    workgroups whose waves pull strided 64-unit batches where one workgroup
+//    fills a CU (Cfg::PERS, b42..80 fields of >= 2 rounds).
+//
 // The kernel is issue-bound on VALU and LDS together: b40 per n is 13 random
-// 8-byte LDS lookups (≈7 LDS cycles each per wave) and ≈105 VALU ops; see
-// DESIGN.md §3.1 for the cycle model and the measured roofline.
+// 8-byte LDS lookups (≈5 LDS cycles each per wave) and ≈78 VALU instructions
+// per wave-step; see DESIGN.md §3.1 for the cycle model and the measured
+// roofline.
 #pragma once
 #include <stdlib.h>
 
