@@ -440,11 +440,12 @@ def test_big_field_kernel_equals_small_field_kernel(ctx, base):
     assert all(O.num_unique_digits(n, base) == u for n, u in l)
 
 
-@pytest.mark.parametrize("base", [55, 58, 65, 67, 68])
+@pytest.mark.parametrize("base", [42, 45, 49, 55, 58, 59, 64, 65, 67, 68])
 def test_persistent_grid_equals_rounds(ctx, base):
     """Bases whose big-field kernel holds one workgroup per CU run fields of
-    >= 2 rounds on the persistent grid (waves pull strided 64-unit batches);
-    1e8 windows (< 2 rounds) run in rounds of workgroups.  A 1e9 field must
+    >= 2 rounds on the persistent grid (waves pull strided 64-unit batches;
+    1024-thread workgroups); 1e8 windows (< 2 rounds) run in rounds of
+    workgroups (b42..50 and b59..64 at 512 threads).  A 1e9 field must
     equal the sum of its ten 1e8 windows, and every near-miss recomputes by
     the oracle.  (b52-54 and b80 1e9 are pinned to oracle fixtures in
     test_fd_bases_whole_fields_1e9.)"""
