@@ -12,4 +12,3 @@ $S pmc sq "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_
 $S pmc fetch "FETCH_SIZE"
 $S pmc write "WRITE_SIZE"
 timeout -k 10 300 python3 -u scripts/bench_configs.py --bases all > gpurun_out/configs.jsonl 2> gpurun_out/configs.err
-timeout -k 10 120 python3 -u scripts/fd2_stamps.py 80:1e6 40:1e6 > gpurun_out/stamps.log 2>&1
