@@ -14,6 +14,11 @@
 //      stored limb, two immediate offsets)
 //   6  ds_read_b64 stride 8 + ds_read_u16 stride 8 (two 51 KB regions)
 //   7..9  the single reads of 5 and 6 alone
+//   10 ds_read_b96 of a 12-byte entry (77 KB, 4-byte aligned: gfx950 DS
+//      unaligned access), checked against a host recomputation
+//   11 ds_read_b96 of a 16-byte entry (aligned)
+//   12 ds_read_b64 stride 8 + ds_read_b32 stride 4 (two regions, 51 + 26 KB)
+//   13 12-byte entries read as ds_read_b64 at +0 and ds_read_b32 at +8
 // Prints ns and LDS-cycles per wave-lookup (clock from s_memtime), so the
 // conflict cost of each layout is measured, not modelled.
 //   hipcc --offload-arch=gfx950 -O3 -o lds_lookup lds_lookup.hip && ./lds_lookup
@@ -22,6 +27,7 @@
 #include <stdio.h>
 
 #define ITERS 2048
+typedef uint32_t v3u __attribute__((ext_vector_type(3)));
 constexpr uint32_t NE = 6400;
 
 template <int MODE>
@@ -66,6 +72,19 @@ __global__ void __launch_bounds__(1024) kern(uint32_t *out, uint64_t *cyc, uint3
             m2 |= *(const uint16_t *)(t + e * 8);
         } else if constexpr (MODE == 9) {  // u16 stride 16 only
             m2 |= *(const uint16_t *)(t + e * 16 + 8);
+        } else if constexpr (MODE == 10) {  // 12-B entries, one ds_read_b96
+            const v3u v = *(const v3u *)__builtin_assume_aligned(t + e * 12, 4);
+            m0 |= v.x; m1 |= v.y; m2 |= v.z;
+        } else if constexpr (MODE == 11) {  // 16-B entries, ds_read_b96
+            const v3u v = *(const v3u *)(t + e * 16);
+            m0 |= v.x; m1 |= v.y; m2 |= v.z;
+        } else if constexpr (MODE == 12) {  // b64 stride 8 + b32 stride 4
+            const uint2 v = *(const uint2 *)(t + e * 8);
+            m0 |= v.x; m1 |= v.y; m2 |= *(const uint32_t *)(t + NE * 8 + e * 4);
+        } else if constexpr (MODE == 13) {  // 12-B entries: b64 at +0, b32 at +8
+            const uint2 v = *(const uint2 *)__builtin_assume_aligned(t + e * 12, 4);
+            asm volatile("" ::"v"(v.x));
+            m0 |= v.x; m1 |= v.y; m2 |= *(const uint32_t *)(t + e * 12 + 8);
         } else {
             const uint32_t d = __umulhi(x, 80);
             const uint4 v = *(const uint4 *)(t + (d * 16 + (lane & 15)) * 16);
@@ -100,6 +119,23 @@ static void run(const char *name, uint32_t *out, uint64_t *cyc, int cus) {
     // per CU: 16 waves x ITERS lookups share the CU's one LDS pipe
     const double per = s / (16.0 * ITERS);
     printf("%-44s %8.3f ms  %6.2f cycles per wave-lookup per CU (s_memtime)\n", name, ms, per);
+    if (MODE == 10) {  // the unaligned b96 read returns the right words
+        static uint32_t o[1024];
+        hipMemcpy(o, out, sizeof o, hipMemcpyDeviceToHost);
+        int bad = 0;
+        for (uint32_t tid = 0; tid < 1024; tid++) {
+            uint32_t x = 2u * 747796405u + tid * 2891336453u + 0u, m0 = 0, m1 = 0, m2 = 0;
+            for (int i = 0; i < ITERS; i++) {
+                x = x * 1664525u + 1013904223u;
+                const uint32_t e = (uint32_t)(((uint64_t)x * NE) >> 32);
+                m0 |= (e * 3) * 2654435761u;
+                m1 |= (e * 3 + 1) * 2654435761u;
+                m2 |= (e * 3 + 2) * 2654435761u;
+            }
+            bad += o[tid] != (m0 ^ m1 ^ m2);
+        }
+        printf("  b96 unaligned check: %d of 1024 lanes differ\n", bad);
+    }
 }
 
 int main() {
@@ -119,6 +155,10 @@ int main() {
     run<7>("b64 stride 16 only", out, cyc, cus);
     run<8>("u16 stride 8 only", out, cyc, cus);
     run<9>("u16 stride 16 only", out, cyc, cus);
+    run<10>("b96 12-B entries (unaligned)", out, cyc, cus);
+    run<11>("b96 16-B entries", out, cyc, cus);
+    run<12>("b64 stride 8 + b32 stride 4", out, cyc, cus);
+    run<13>("12-B entries: b64 +0 and b32 +8", out, cyc, cus);
     printf("rc=%d\n", (int)hipGetLastError());
     return 0;
 }
