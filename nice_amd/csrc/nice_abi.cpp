@@ -1047,6 +1047,8 @@ static uint64_t env_msd_floor() {
     return v;
 }
 
+}  // extern "C"
+
 // The reference GPU path's AdaptiveFloor (client_process_gpu.rs:96-184),
 // selected by msd_floor = NICE_MSD_FLOOR_ADAPTIVE.  Process-wide, like the
 // reference's OnceLock: NICE_GPU_MSD_FLOOR pins it (no adaptation); otherwise
@@ -1091,6 +1093,8 @@ AdaptiveFloor &adaptive_floor() {  // call under g_af_mu
     return af;
 }
 }  // namespace
+
+extern "C" {
 
 double nice_adaptive_floor_step(double floor, double msd_seconds, double total_seconds) {
     const double gpu_tail = std::max(0.0, total_seconds - msd_seconds);
