@@ -1,4 +1,5 @@
-"""Multi-rank plumbing of bench.py on CPU (gloo, world_size 2): weak-scaling
+"""Multi-rank plumbing of bench.py on CPU (gloo, world_size 2; one 8-rank
+rehearsal of the N = 8 path): weak-scaling
 field assignment (disjoint consecutive 1e9 fields, all inside base 40's range)
 and the max-over-ranks timing reduction."""
 import os
@@ -243,6 +244,61 @@ def test_two_rank_field_sharding_matches_single_process():
     assert list(D.dealt_chunks(0, 10, 3, 2, 1)) == [(3, 6), (9, 10)]
     assert D.shard_bounds(0, 10, 1, 3) == (4, 7)
     assert D.client_chunk_size(10 ** 9) == 10 ** 6 and D.client_chunk_size(10 ** 13) == 10 ** 8
+
+
+def _eight_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from nice_amd import dist as D
+    from nice_amd.types import FieldSize
+    res = {}
+    r = D.process_range_detailed_dist(FieldSize(10 ** 6, 10 ** 6 + 4_001), 10, shard_fn=_oracle_detailed_shard)
+    res["b10_oob"] = ([(d.num_uniques, d.count) for d in r.distribution],
+                      [(n.number, n.num_uniques) for n in r.nice_numbers])
+    r = D.process_range_niceonly_dist(FieldSize(47, 100), 10, shard_fn=_oracle_niceonly_shard)
+    res["nice_b10"] = [(n.number, n.num_uniques) for n in r.nice_numbers]
+    # bench.py's step at N = 8: the field pipeline, exchange overlapped, with
+    # fields smaller than the world (most ranks' shards empty) between others
+    pipe = D.FieldPipeline(_OracleCtx(), _OracleCtx(), dist, chunk_size=97)
+    fields = [(FieldSize(47, 1_047), 10), (FieldSize(69, 70), 10), (FieldSize(1, 5), 12),
+              (FieldSize(10 ** 6, 10 ** 6 + 1_003), 40), (FieldSize(2 * 10 ** 6, 2 * 10 ** 6 + 777), 10)]
+    got = [pipe.step(f, b) for f, b in fields]
+    got = [g for g in got if g is not None] + pipe.drain()
+    res["field_pipeline"] = [((r.range_start, r.range_end),
+                              [(d.num_uniques, d.count) for d in det.distribution],
+                              [(n.number, n.num_uniques) for n in det.nice_numbers],
+                              [n.number for n in nic.nice_numbers]) for r, det, nic, _ in got]
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def test_eight_rank_rehearsal():
+    """The N = 8 code path (the driver's scaling run) rehearsed on CPU: eight
+    gloo ranks shard detailed fields, deal niceonly chunks and run bench.py's
+    field pipeline, including fields smaller than the world; every rank ends
+    with the whole field's results, equal to the oracle's."""
+    from oracle import oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_eight_worker, args=(r, 8, port, q)) for r in range(8)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(out[r] == out[0] for r in range(8))
+    w = O.process_range_detailed(10 ** 6, 10 ** 6 + 4_001, 10)
+    assert out[0]["b10_oob"] == (w.distribution, w.nice_numbers)
+    assert out[0]["nice_b10"] == [(69, 10)]
+    want = [((47, 1_047), 10), ((69, 70), 10), ((1, 5), 12), ((10 ** 6, 10 ** 6 + 1_003), 40),
+            ((2 * 10 ** 6, 2 * 10 ** 6 + 777), 10)]
+    assert [r[0] for r in out[0]["field_pipeline"]] == [f for f, _ in want]
+    for ((a, b), base), (_, d, near, nice) in zip(want, out[0]["field_pipeline"]):
+        w = O.process_range_detailed(a, b, base)
+        assert (d, near) == (w.distribution, w.nice_numbers), (a, base)
+        assert nice == _oracle_niceonly_shard(a, b, base, 97), (a, base)
 
 
 def test_both_modes_runner_matches_sequential_and_propagates_errors():
