@@ -372,3 +372,45 @@ def test_adaptive_floor_seed_and_pin():
     assert 250 <= f <= 256_000 and f >= min(256_000.0, 512_000.0 / cpus)  # cgroup quota can only lower cores
     assert run("64000")[:2] == (64000.0, 0xFFFFFFFF)
     assert run("bogus")[1] == 3
+
+
+# --- a plain C host of the boundary (examples/nice_field.c) -------------------
+def build_c_example():
+    """gcc -std=c99 -pedantic -Werror against include/nice_hip.h alone, linked
+    to libnice_hip.so: the header is self-contained C and the symbols resolve."""
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "examples")], check=True)
+    return os.path.join(ROOT, "examples", "nice_field")
+
+
+def run_c_example(*args):
+    import subprocess
+    r = subprocess.run([build_c_example(), *map(str, args)], capture_output=True, text=True, timeout=300)
+    dist, nice = [], []
+    for line in r.stdout.splitlines():
+        w = line.split()
+        if w[0] == "dist":
+            dist.append((int(w[1]), int(w[2])))
+        elif w[0] == "nice":
+            nice.append((int(w[1]), int(w[2])))
+    return r.returncode, dist, nice, r.stderr
+
+
+def test_c_host_example_cpu_mode(golden):
+    """The reference's golden vectors through a C host calling the CPU API
+    (the client without --gpu): b10 whole range, b40 / b80 first 1e4."""
+    for c in golden["reference"]["detailed"]:
+        size = [c["size"]] if c["size"] else []
+        rc, dist, nice, err = run_c_example("detailed", c["base"], "range", *size)
+        assert rc == 0, err
+        assert dist == [tuple(x) for x in c["distribution"]], c["source"]
+        assert nice == [tuple(x) for x in c["nice_numbers"]], c["source"]
+    rc, _, nice, err = run_c_example("niceonly", 10, "range")
+    assert rc == 0 and nice == [(69, 10)], err
+    rc, _, nice, _ = run_c_example("detailed", 10, 47, 100)
+    assert (69, 10) in nice
+    # --gpu never falls back to the CPU: without a device it is an error
+    n = ctypes.c_int(-1)
+    if _lib.lib().nice_device_count(ctypes.byref(n)) != 0 or n.value == 0:
+        rc, dist, nice, err = run_c_example("--gpu", "detailed", 10, "range")
+        assert rc == 4 and not dist and "device" in err

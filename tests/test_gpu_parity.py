@@ -773,3 +773,24 @@ def test_massive_whole_field_sums():
         assert (got_c, got_r) == (tot_c, tot_r)
     finally:
         c.close()
+
+
+def test_c_host_example_gpu():
+    """A plain C host (examples/nice_field.c: include/nice_hip.h + the .so, no
+    Python in the process) through the GPU entry points: the default b40 and
+    hi-base b80 1e6 fields against the oracle, b10 niceonly, and an
+    out-of-range b10 field whose 5 395 near-misses outgrow the host's first
+    list capacity (the NICE_ERR_CAPACITY retry the header prescribes)."""
+    from test_abi import run_c_example
+    for base in (40, 80):
+        s, _ = O.base_range(base)
+        rc, dist, nice, err = run_c_example("--gpu", "detailed", base, "range", 10 ** 6)
+        assert rc == 0, err
+        want = O.process_range_detailed(s, s + 10 ** 6, base)
+        assert (dist, nice) == (want.distribution, want.nice_numbers), base
+    rc, dist, nice, err = run_c_example("--gpu", "detailed", 10, 10 ** 6, 10 ** 6 + 10 ** 4)
+    assert rc == 0, err
+    want = O.process_range_detailed(10 ** 6, 10 ** 6 + 10 ** 4, 10, cap=10 ** 4)
+    assert (dist, nice) == (want.distribution, want.nice_numbers) and len(nice) == 5395
+    rc, _, nice, err = run_c_example("--gpu", "niceonly", 10, "range")
+    assert rc == 0 and nice == [(69, 10)], err
