@@ -794,3 +794,20 @@ def test_c_host_example_gpu():
     assert (dist, nice) == (want.distribution, want.nice_numbers) and len(nice) == 5395
     rc, _, nice, err = run_c_example("--gpu", "niceonly", 10, "range")
     assert rc == 0 and nice == [(69, 10)], err
+
+
+def test_fd_kernel_fuzz_windows(ctx):
+    """Seeded fuzz over every FD base: 64 windows at random offsets inside
+    the valid range with sizes spread log-uniformly over 1 .. 3e6 (tails,
+    single rounds, several rounds, the small-field chunking), each against
+    the oracle (client-chunked, 8 threads)."""
+    rng = random.Random(20261017)
+    bases = list(range(40, 69)) + [80]
+    bases = [b for b in bases if N._lib.lib().nice_fd_kernel_base(b) == 1]
+    for i in range(64):
+        base = bases[i % len(bases)] if i < len(bases) else rng.choice(bases)
+        s, e = O.base_range(base)
+        size = max(1, int(10 ** rng.uniform(0, 6.48)))
+        a = s + rng.randrange(e - s - size)
+        want = O.process_field_detailed_mt(a, a + size, base, 8, cap=size)
+        check_detailed(ctx, a, a + size, base, want=want)
