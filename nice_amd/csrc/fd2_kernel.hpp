@@ -143,6 +143,33 @@ constexpr bool fits64(unsigned base, int digits) {
     return true;
 }
 
+// Limbs decoded by VALU instead of a table lookup (Cfg::VD: top C limbs +
+// 16 x top S limbs), per base where the lookups' bank conflicts outweigh the
+// VALU work: the best of VD 0/1/2/3/17 on the 1e9 field at the range start
+// (scripts/vd_sweep_all.py, profiles/r02/vd_sweep_all.log), kept where it
+// gains over ~1 %; without a low-digit table also limb 0 (VD & 256,
+// profiles/r02/vd_sweep_low.log).  b64: 6.31 -> 4.25 ms (its table index
+// n^2 mod 4096 keeps few residues mod 32, so lookups pile onto few banks);
+// b45 2.60 -> 2.41; b60 3.79 -> 3.41; b63 3.96 -> 3.70; b68 7.42 -> 6.87;
+// b80 8.22 -> 7.46; b40 neutral (r01).  Re-swept on the persistent grid
+// (profiles/r03/vd_sweep_persistent.log): b55 0 -> 1 (2.91 -> 2.87 ms), b58
+// 1 -> 2 (3.08 -> 3.00); every other base within ~1 % of its choice.
+constexpr int valu_limbs(int base) {
+    switch (base) {
+    case 43: case 44: case 45: case 48: case 50: case 54: case 55: return 1;
+    case 53: case 58: case 65: return 2;
+    case 67: case 68: case 80: return 256;  // limb 0 by VALU
+    // b59..64: the low-digit table with its carries in a side table (VD &
+    // 1024, Cfg::LSDX), then the best top limbs by VALU: b59 3.31 -> 3.01 ms,
+    // b60 3.39 -> 3.18, b62 3.49 -> 3.35, b63 3.71 -> 3.59, b64 4.17 -> 4.13
+    // (profiles/r03/lsdx_sweep.log)
+    case 59: case 63: case 64: return 1024 + 2;
+    case 60: return 1024 + 17;
+    case 62: return 1024 + 1;
+    default: return 0;
+    }
+}
+
 // LDS bytes / waves per SIMD of a base's kernel at a workgroup size (the
 // formulas of Cfg, evaluated without instantiating it).
 constexpr int lds_bytes(int base, int wg) {
@@ -153,8 +180,10 @@ constexpr int lds_bytes(int base, int wg) {
     const int tb0 = (window_w(base) * (wg / 2) * 4 + 4 * (base + 1) + 15) / 16 * 16;
     const int tb = tb0 >= ebt ? tb0 : (ebt + 15) / 16 * 16;
     const int db = base - 32;
-    const bool lsd = mw == 2 && db > 0 && db + (db > 20 ? 4 : 10) <= 30;
-    return tb + (b2 * es + 15) / 16 * 16 + (lsd ? (2 * b2 * es + 15) / 16 * 16 : 0);
+    const bool lsd_w1 = mw == 2 && db > 0 && db + (db > 20 ? 4 : 10) <= 30;
+    const bool lsdx = mw == 2 && db > 0 && !lsd_w1 && (valu_limbs(base) & 1024) != 0;
+    return tb + (b2 * es + 15) / 16 * 16 + (lsd_w1 || lsdx ? (2 * b2 * es + 15) / 16 * 16 : 0) +
+           (lsdx ? (2 * b2 + 15) / 16 * 16 : 0);
 }
 // Waves per SIMD actually resident: the LDS and VGPR caps, in whole
 // workgroups (a workgroup puts wg / 256 waves on each SIMD).
@@ -258,20 +287,28 @@ struct Cfg {
     // extra multiply-add per step); wider bases have no low-digit table.
     static constexpr int DB = BASE - 32;
     static constexpr bool TIGHT = DB > 20;
-    static constexpr bool LSD = MW == 2 && DB > 0 && DB + (TIGHT ? 4 : 10) <= 30;
+    static constexpr bool LSD_W1 = MW == 2 && DB > 0 && DB + (TIGHT ? 4 : 10) <= 30;
+    // VD & 1024 (probe A/B, b59..64: word 1 of the entry is all digit bits):
+    // the low-digit table with the carries and wrap flags in a side table of
+    // bytes (bit 0 the S carry, bits 1-3 the C carry, bit 6 / 7 the D1 / N3
+    // wraps), read at rc = TK + n mod B + i; r8 then holds TL too (TL can
+    // pass the 16-bit immediate offset).
+    static constexpr bool LSDX = MW == 2 && DB > 0 && !LSD_W1 && (VD_ & 1024) != 0;
+    static constexpr bool LSD = LSD_W1 || LSDX;
     // (regions padded to 16 bytes: the image is copied in with 16-byte accesses)
     static constexpr int TL = TB + ((int)(B * ES) + 15) / 16 * 16;  // low-digit table (2B entries)
+    static constexpr int TK = TL + (LSD ? ((int)(2 * B * ES) + 15) / 16 * 16 : 0);  // LSDX: carry bytes
     static constexpr int TEND = SPLIT ? (TH + (int)(B * ES) + 15) / 16 * 16
-                                      : TL + (LSD ? ((int)(2 * B * ES) + 15) / 16 * 16 : 0);
+                                      : TK + (LSDX ? ((int)(2 * B) + 15) / 16 * 16 : 0);
     static constexpr int HB = SPLIT ? TEND : 0;  // window rows
     static constexpr int LDS_BYTES = SPLIT ? HB + HIST_BYTES : TEND;
     static constexpr int TAB_BYTES = TEND - TC0;  // table image copied in per workgroup
     static constexpr int ZA = SPLIT ? TC0 : TB;   // zeroed per workgroup: [0, ZA) and [HB, LDS_BYTES)
     static constexpr int LO = LSD ? 1 : 0;  // first stored / looked-up limb
     static constexpr u32 DMASK = (1u << (DB > 0 && DB < 32 ? DB : 0)) - 1;
-    static constexpr u32 FLAG_D1 = 1u << 30, FLAG_N3 = 1u << 31;  // any flag: w1 >= FLAG_D1
-    static constexpr int F0 = TIGHT ? DB : (DB + 3) / 4 * 4;
-    static constexpr int FC = TIGHT ? DB + 1 : F0 + 4;
+    static constexpr u32 FLAG_D1 = LSDX ? 1u << 6 : 1u << 30, FLAG_N3 = LSDX ? 1u << 7 : 1u << 31;  // any flag: w1 >= FLAG_D1
+    static constexpr int F0 = LSDX ? 0 : TIGHT ? DB : (DB + 3) / 4 * 4;
+    static constexpr int FC = LSDX ? 1 : TIGHT ? DB + 1 : F0 + 4;
     static constexpr int F0W = TIGHT ? 1 : 4, FCW = TIGHT ? 3 : 6;  // field widths
     // C += 3S + N3 (N3 = 3n + 1, NN limbs).  A C limb sum is < 5B, so its
     // carry (0..4) is a multiply-high by MAGIC = ceil(2^32 / (ES B)) (exact
@@ -318,7 +355,8 @@ struct Cfg {
     static constexpr bool VDL = (VD & 256) != 0 && !LSD;
     static constexpr u32 MAGIC_D = (u32)(((1ull << 32) + ES * BASE - 1) / (ES * BASE));
     static_assert(VD == 0 || (MW >= 2 && split_exact(BASE, ES, MAGIC_D)), "VALU digit split");
-    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1 && (VD & ~0x3ff) == 0,
+    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1 && (VD & ~0x7ff) == 0 &&
+                      ((VD & 1024) == 0 || LSDX),
                   "VALU-decoded limbs");
     // Waves per SIMD: what the LDS allows, capped by what the lane state
     // needs in VGPRs (the register budget is set to match, see state_waves).
@@ -330,13 +368,13 @@ struct Cfg {
     static_assert(SL < NS && CL < NC && EL <= NE, "FD layout needs cached high limbs");
     static_assert(ND <= NX + 1 && NE2 <= NX + 1 && NE <= NS + 1, "difference limb counts");
     static_assert(S_TOPD >= 1 && C_TOPD >= 1, "top limb");
-    static_assert(TB >= (int)EBT && TB - (int)EBT < 65536 && (!LSD || TL < 65536), "LDS offsets");
+    static_assert(TB >= (int)EBT && TB - (int)EBT < 65536 && (!LSD || LSDX || TL < 65536), "LDS offsets");
     static_assert(!SPLIT || (TH < 65536 && TB + (int)(B * ES) == ES << T && 4 * NBINS <= TC0 && TCHUNK <= 255),
                   "split layout");
     static_assert(LDS_BYTES <= 163840, "LDS");
     static_assert((SPLIT || TB % 16 == 0) && TAB_BYTES % 16 == 0 && HB % 16 == 0, "16-byte table copy");
     static_assert(W0 >= 0 && W0 + W <= NBINS, "window");
-    static_assert(!LSD || (ES == 8 && FC + FCW <= 30), "low-digit entry layout");
+    static_assert(!LSD || (ES == 8 && (LSDX ? TIGHT && FC + FCW <= 6 : FC + FCW <= 30)), "low-digit entry layout");
     static_assert(C1 || ((unsigned long long)MAGICB * B - (1ull << 32)) * (TMAX / ES) < (1ull << 32),
                   "C-limb carry magic");
     static_assert(NN <= SL && NE >= NS, "C += 3S + N3 layout");
@@ -367,7 +405,8 @@ struct State {
     u32 C[P::NC];    // n^3: same with CL
     u32 D1[P::ND];   // scaled, plain
     u32 N3[P::NN];   // 3n + 1, scaled, limb i < SL offset by -3 ES BT
-    u32 r8;          // low-digit table byte offset: ES * (n mod B + i)
+    u32 r8;          // low-digit table byte offset: ES * (n mod B + i) (LSDX: + TL)
+    u32 rc;          // LSDX: carry byte address TK + n mod B + i
     u32 hi[P::MW];   // mask of the cached (rarely changing) limbs of S and C
 };
 
@@ -515,7 +554,8 @@ __device__ __forceinline__ void init(State<P> &st, u64 n_lo, u64 n_hi) {
     if constexpr (!P::N64) {
         // wide bases (b80: the 1024-thread kernel at the 128-VGPR cap): u64
         // columns, the layout whose register allocation spills least.
-        st.r8 = X[0] * P::ES;
+        st.r8 = X[0] * P::ES + (P::LSDX ? (u32)P::TL : 0u);
+        st.rc = X[0] + (u32)P::TK;
         {
             u64 acc[2 * P::NX];
 #pragma unroll
@@ -549,7 +589,8 @@ __device__ __forceinline__ void init(State<P> &st, u64 n_lo, u64 n_hi) {
             normalize64<P>(acc, st.N3);
         }
     } else {
-        st.r8 = X[0] * P::ES;
+        st.r8 = X[0] * P::ES + (P::LSDX ? (u32)P::TL : 0u);
+        st.rc = X[0] + (u32)P::TK;
         {  // S = X^2
             A acc[2 * P::NX];
 #pragma unroll
@@ -700,6 +741,7 @@ __device__ __forceinline__ void step(State<P> &st, const unsigned char *smem, u3
     }
     st.S[ST] += cS;
     st.r8 += ES;
+    if constexpr (P::LSDX) st.rc += 1;
     const bool topS = st.S[ST] >= (1u << P::SH), topC = st.C[CT] >= P::DC;
     if constexpr (P::LSD) {
         if (w1 >= P::FLAG_D1 || topS || topC)
@@ -750,13 +792,20 @@ __global__ void fd2_tables_kernel(unsigned char *tb) {
         mark(s0);
         mark(c0);
         const u32 d1 = (2 * e + 1) % B, n3 = (3 * e + 1) % B;
-        v[1] |= d1 + 2 >= B ? P::FLAG_D1 : 0u;                   // D1 limb-0 wrap
-        v[1] |= n3 + 3 >= B ? P::FLAG_N3 : 0u;                   // N3 limb-0 wrap
+        u32 f = 0;
+        f |= d1 + 2 >= B ? P::FLAG_D1 : 0u;                   // D1 limb-0 wrap
+        f |= n3 + 3 >= B ? P::FLAG_N3 : 0u;                   // N3 limb-0 wrap
         const u32 sc = s0 + d1 >= B ? 1u : 0u, cc = (c0 + 3 * s0 + n3) / B;
-        v[1] |= (P::TIGHT ? sc : P::ES * sc) << P::F0;            // S  += D1 carry
-        v[1] |= (P::TIGHT ? cc : P::ES * cc) << P::FC;            // C += 3S + N3 carry
-        put(tb + (P::TL - P::TB) + e * P::ES);
-        put(tb + (P::TL - P::TB) + (e + P::B) * P::ES);
+        f |= (P::TIGHT ? sc : P::ES * sc) << P::F0;            // S  += D1 carry
+        f |= (P::TIGHT ? cc : P::ES * cc) << P::FC;            // C += 3S + N3 carry
+        if constexpr (P::LSDX) {
+            tb[(P::TK - P::TC0) + e] = (unsigned char)f;
+            tb[(P::TK - P::TC0) + e + P::B] = (unsigned char)f;
+        } else {
+            v[1] |= f;
+        }
+        put(tb + (P::TL - P::TC0) + e * P::ES);
+        put(tb + (P::TL - P::TC0) + (e + P::B) * P::ES);
     }
 }
 
@@ -919,10 +968,15 @@ __device__ __forceinline__ void walk_chunk(State<P> &st, const unsigned char *sm
             for (int q = P::LO; q < P::CL; q++) m[q & 1] |= st.C[q];
         } else {
             if constexpr (P::LSD) {
-                const uint2 v = *(const uint2 *)(smem + P::TL + st.r8);
+                const uint2 v = *(const uint2 *)(smem + (P::LSDX ? 0 : P::TL) + st.r8);
                 m[0] |= v.x;
-                m[1] |= v.y & P::DMASK;
-                w1 = v.y;
+                if constexpr (P::LSDX) {
+                    m[1] |= v.y;
+                    w1 = smem[st.rc];
+                } else {
+                    m[1] |= v.y & P::DMASK;
+                    w1 = v.y;
+                }
             }
 #pragma unroll
             for (int q = P::LO; q < P::SL; q++) {
@@ -1269,26 +1323,6 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
 namespace nice {
 namespace fd2 {
 
-// Limbs decoded by VALU instead of a table lookup (Cfg::VD: top C limbs +
-// 16 x top S limbs), per base where the lookups' bank conflicts outweigh the
-// VALU work: the best of VD 0/1/2/3/17 on the 1e9 field at the range start
-// (scripts/vd_sweep_all.py, profiles/r02/vd_sweep_all.log), kept where it
-// gains over ~1 %; without a low-digit table also limb 0 (VD & 256,
-// profiles/r02/vd_sweep_low.log).  b64: 6.31 -> 4.25 ms (its table index
-// n^2 mod 4096 keeps few residues mod 32, so lookups pile onto few banks);
-// b45 2.60 -> 2.41; b60 3.79 -> 3.41; b63 3.96 -> 3.70; b68 7.42 -> 6.87;
-// b80 8.22 -> 7.46; b40 neutral (r01).  Re-swept on the persistent grid
-// (profiles/r03/vd_sweep_persistent.log): b55 0 -> 1 (2.91 -> 2.87 ms), b58
-// 1 -> 2 (3.08 -> 3.00); every other base within ~1 % of its choice.
-constexpr int valu_limbs(int base) {
-    switch (base) {
-    case 43: case 44: case 45: case 48: case 50: case 54: case 55: return 1;
-    case 53: case 58: case 63: case 65: return 2;
-    case 60: case 62: case 67: case 68: case 80: return 256;  // limb 0 by VALU
-    case 64: return 258;
-    default: return 0;
-    }
-}
 
 }  // namespace fd2
 }  // namespace nice

@@ -41,6 +41,18 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
         case 358: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 258>>(p, num_cus, s);
         default: break;
         }
+        // Low-digit table with a side table of carries (Cfg::LSDX, b59..64):
+        // NICE_FD2_VD = 1100 + VD, VD = the VALU-decoded top limbs
+        constexpr int DB_ = B_ - 32;
+        if constexpr ((B_ + 31) / 32 == 2 && DB_ > 0 && DB_ + (DB_ > 20 ? 4 : 10) > 30) {
+            switch ((int)probe_knob("NICE_FD2_VD", 0)) {
+            case 1100: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 1024>>(p, num_cus, s);
+            case 1101: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 1025>>(p, num_cus, s);
+            case 1102: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 1026>>(p, num_cus, s);
+            case 1117: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 1041>>(p, num_cus, s);
+            default: break;
+            }
+        }
         // Persistent grid A/B (NICE_FD2_PERS = 1: on, 2: off; 3 / 4: 1024-thread
         // workgroups with / without it, where the LDS and VGPRs allow one)
         if constexpr (waves_at(B_, 1024) >= 4) {
@@ -76,8 +88,11 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
             }
         }
 #endif
-        return wg512 ? launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, valu_limbs(B_)>>(p, num_cus, s)
-                     : launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), valu_limbs(B_)>>(p, num_cus, s);
+        // (the LSDX bases' tables leave room for one workgroup per CU: 1024
+        // threads for every field size, 4 waves per SIMD instead of 2)
+        constexpr bool small512 = (valu_limbs(B_) & 1024) == 0;
+        return wg512 && small512 ? launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, valu_limbs(B_)>>(p, num_cus, s)
+                                 : launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), valu_limbs(B_)>>(p, num_cus, s);
     }
 }
 
