@@ -49,7 +49,9 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
             case 1100: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 1024>>(p, num_cus, s);
             case 1101: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 1025>>(p, num_cus, s);
             case 1102: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 1026>>(p, num_cus, s);
+            case 1103: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 1027>>(p, num_cus, s);
             case 1117: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 1041>>(p, num_cus, s);
+            case 1118: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 1042>>(p, num_cus, s);
             default: break;
             }
         }
