@@ -99,40 +99,32 @@ def parse():
     return p.parse_args()
 
 
-TRAFFIC_FILES = ("profiles/r02/traffic.json", "profiles/r01/traffic.json")
+PMC_BENCH_FILE = "profiles/r04/pmc_bench.json"
 
 
-def pmc_traffic():
-    """HBM bytes per launch of the detailed kernel on the 1e9 b40 field: from
-    the PMC passes of this bench command (profiles/r03/pmc_bench.json,
-    FETCH_SIZE x2 + WRITE_SIZE), else the older detailed-only passes
-    (scripts/traffic_json.py); (bytes, file) or (None, None)."""
-    hw = pmc_bench()
-    if hw is not None and "traffic_bytes" in hw[0]:
-        return hw[0]["traffic_bytes"], hw[1]
-    for rel in TRAFFIC_FILES:
-        try:
-            with open(os.path.join(ROOT, rel)) as f:
-                return json.load(f)["bytes_per_launch"], rel
-        except (OSError, KeyError, ValueError):
-            continue
-    return None, None
-
-
-PMC_BENCH_FILES = ("profiles/r03/pmc_bench.json",)
+def lib_sha16() -> str:
+    """First 16 hex digits of sha256 of the library this process loads."""
+    import hashlib
+    from nice_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
 def pmc_bench():
     """Counter-derived figures of the fd2 kernel from the committed rocprofv3
-    --pmc passes of this bench command (scripts/pmc_bench.py); (derived, file)
-    or None."""
-    for rel in PMC_BENCH_FILES:
-        try:
-            with open(os.path.join(ROOT, rel)) as f:
-                return json.load(f)["derived"], rel
-        except (OSError, KeyError, ValueError):
-            continue
-    return None
+    --pmc passes of this bench command (scripts/pmc_bench.py): (derived, file,
+    status).  The passes record the sha256 of the library they profiled;
+    status is "current" only when it equals the loaded library's, else
+    "stale" and derived is None (counter figures of another build are not
+    reported as this one's)."""
+    try:
+        with open(os.path.join(ROOT, PMC_BENCH_FILE)) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, PMC_BENCH_FILE, "missing"
+    if d.get("lib_sha16") != lib_sha16():
+        return None, PMC_BENCH_FILE, f"stale (profiled library {d.get('lib_sha16')}, loaded {lib_sha16()})"
+    return d.get("derived"), PMC_BENCH_FILE, "current"
 
 
 def rank_field(base_start: int, rank: int, size: int = FIELD_SIZE):
@@ -246,8 +238,7 @@ def cpu_baseline(start, target_s, base=BASE, field=FIELD_SIZE):
             "detailed_numbers_per_sec": det_rate, "niceonly_numbers_per_sec": nice_rate}
 
 
-def main():
-    args = parse()
+def main(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -488,40 +479,46 @@ def main():
             "bound": "valu", "kernel": f"nice::fd2::fd2_kernel<Cfg<{base}, ...>>",
             "achieved": achieved, "peak": PEAK_INT32_TOPS, "unit": "int32 Tops/s",
             "frac": achieved / PEAK_INT32_TOPS,
-            "traffic": pmc_traffic()[0] if default_cfg and world == 1 else None,
-            "traffic_source": pmc_traffic()[1] if default_cfg and world == 1 else None,
+            "traffic": None,
             "kernel_ms": kms, "numbers_per_launch": shard,
             "work_per_unit": f"{w_alg} int32 ops per n (4 per digit x {base} digits, SURVEY 8d)",
+            "frac_is": "W_alg model (SURVEY 8d charges a division-per-digit kernel 4 int32 ops per "
+                       "digit); this kernel does the digit work in fewer instructions, partly as LDS "
+                       "table lookups, so frac is NOT a hardware utilisation and can pass 1. The "
+                       "hardware bound is hw_bound: the busier of the VALU and LDS pipes, from the "
+                       "rocprofv3 --pmc passes of this command on this library",
             "step_frac": step_rate / PEAK_INT32_TOPS,
             "pipelined_launch_span_ms": pipelined_kms,
             "note": "integer-VALU/LDS bound (no HBM stream, no contraction). kernel_ms = median "
                     "duration of this rank's detailed shard launched alone (HIP events on its "
                     "launch stream, after the timed region; the same dispatches close the rocprofv3 "
                     "trace of this command). step_frac = the same work per timed step, both modes "
-                    "and the pipeline's overlap of consecutive fields included (it can pass 1: the "
-                    "SURVEY 8d charge of 4 int32 ops per digit is a model of a division-per-digit "
-                    "kernel, and this one does the digit work in fewer instructions, partly as LDS "
-                    "table lookups). frac_hw / hw: what the hardware counters of this command show "
-                    "(committed rocprofv3 --pmc passes). traffic: HBM bytes per launch "
-                    "(traffic_source, FETCH_SIZE x2 + WRITE_SIZE); the field's bounds are the only "
-                    "input",
+                    "and the pipeline's overlap of consecutive fields included. traffic: HBM bytes "
+                    "per launch (FETCH_SIZE x2 + WRITE_SIZE); the field's bounds are the only input",
         }
-        hw = pmc_bench() if default_cfg and world == 1 else None
-        if hw is not None:
-            der, src = hw
-            line["roofline"]["frac_hw"] = der.get("valu_busy")
-            line["roofline"]["hw"] = {
-                "source": src, "valu_busy": der.get("valu_busy"),
-                "valu_lane_ops_per_n": der.get("valu_lane_ops_per_n"),
-                "valu_issue_frac": der["valu_lane_ops_per_n"] * shard / (kms / 1e3) / 1e12
-                / PEAK_INT32_TOPS if "valu_lane_ops_per_n" in der else None,
-                "lds_instr_per_n": der.get("lds_instr_per_n"),
-                "lds_conflict_frac": der.get("lds_conflict_frac"),
-                "note": "frac_hw = VALUBusy of the fd2 kernel (rocprofv3 --pmc passes of this "
-                        "bench command); valu_issue_frac = executed VALU lane-ops (SQ_INSTS_VALU x "
-                        "64) per second of kernel_ms over the 32-lanes/clk peak: the SIMDs issue "
-                        "many int ops at half rate (profiles/r01/isa_issue_rates_gfx950.log) and "
-                        "the LDS lookups replace most of the per-digit VALU work"}
+        if default_cfg and world == 1:
+            der, src, status = pmc_bench()
+            line["roofline"]["hw_source"] = src
+            line["roofline"]["hw_status"] = status
+            if der is not None:
+                vb, lb = der.get("valu_busy"), der.get("lds_busy")
+                line["roofline"]["traffic"] = der.get("traffic_bytes")
+                line["roofline"]["hw"] = {
+                    "valu_busy": vb, "lds_busy": lb,
+                    "lds_conflict_frac": der.get("lds_conflict_frac"),
+                    "lds_cycles_per_instr": der.get("lds_cycles_per_instr"),
+                    "valu_lane_ops_per_n": der.get("valu_lane_ops_per_n"),
+                    "lds_instr_per_n": der.get("lds_instr_per_n"),
+                    "kernel_cycles": der.get("kernel_cycles"),
+                    "note": "valu_busy = VALUBusy/100 (SQ_ACTIVE_INST_VALU / CUs / kernel cycles; it "
+                            "can pass 1 with the fast-issue integer ops, profiles/r01/"
+                            "isa_issue_rates_gfx950.log); lds_busy = SQ_LDS_IDX_ACTIVE / CUs / kernel "
+                            "cycles (the CU's one LDS pipe); lds_conflict_frac = SQ_LDS_BANK_CONFLICT / "
+                            "SQ_LDS_IDX_ACTIVE; kernel cycles = GRBM_GUI_ACTIVE / XCDs"}
+                if vb is not None and lb is not None:
+                    pipe, busy = ("valu", vb) if vb >= lb else ("lds", lb)
+                    line["roofline"]["hw_bound"] = {"pipe": pipe, "busy": busy}
+                    line["roofline"]["frac_hw"] = busy
     st = last_stats[0]
     if st is not None:
         line["niceonly"] = {"ranges": st.ranges, "range_numbers": st.range_numbers,
@@ -546,5 +543,37 @@ class _Skip:
         return None
 
 
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` (N > 1) without a distributed launcher: start one -- as a
+    CHILD process, before this process has touched a GPU (bench.py initialises
+    HIP only inside main()) -- running this same command line with N ranks,
+    one per GPU, on 127.0.0.1 and a free port.  Rank 0's JSON line reaches
+    stdout through the inherited descriptor; the exit status is the child's."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def entry() -> int:
+    args = parse()
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            return spawn_ranks(args.gpus)
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE="
+              f"{os.environ['WORLD_SIZE']} ranks", file=sys.stderr)
+        return 2
+    main(args)
+    return 0
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(entry())

@@ -1110,7 +1110,11 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
     }
     State<P> st;
     if (active) init<P>(st, n0_lo, n0_hi);
-    __syncthreads();  // drains the DMA (vmcnt(0)) before the barrier
+    // The table DMA must have landed before any wave reads LDS: wait for it
+    // explicitly (a workgroup barrier alone need not imply vmcnt(0)), then
+    // the barrier.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     FD2_STAMP(a, 1);  // state built, tables in LDS
 
     // Window counters: row u - W0, column tid mod HROW (u16 halves / u8 quarters).
@@ -1241,33 +1245,51 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
     DetailedLaunch q = p;
     u64 left = p.count;
     while (left) {
-        const u64 cnt = left < max_count ? left : max_count;
-        // Chunk floor for fields too small to fill the chip: a lane's init
-        // costs about ten steps, but with idle CUs latency wins (b40 1e6:
-        // kernel 25 us at a floor of 32, 14 us at 4; scripts/small_fields.py).
-        const u64 min_chunk = probe_knob("NICE_FD2_MINCHUNK", 4);
-        // Whole rounds of workgroups, chunks <= the target (and <= B, the
-        // low-digit table's reach).
-        u64 rounds = (cnt + tchunk * lanes - 1) / (tchunk * lanes);
-        if (rounds < 1) rounds = 1;
-        u64 chunk = (cnt + rounds * lanes - 1) / (rounds * lanes);
-        if (chunk < min_chunk) chunk = cnt < min_chunk ? cnt : min_chunk;
-        if (chunk < 1) chunk = 1;
-        // Odd chunks: lane l of a wave then sits at n mod B = r0 + chunk * l,
-        // so its low-digit entries fall on 32 distinct bank pairs per
-        // half-wave (B is a multiple of 32 for the LSD bases).  Without a
-        // low-digit table (b80) limb 0 of n^2 and n^3 is looked up in the
-        // pair table, and a chunk divisible by 16 puts a 16-lane group on
-        // ONE bank quad for those lookups (n^2 mod 16 equal on every lane):
-        // b80 1e9 at chunk 2544 took 11.8 ms, at 2545 9.3.
-        if (chunk > 1 && (P::LSD ? chunk % 2 == 0 : chunk % 16 == 0)) chunk++;
-        if (chunk > P::B) chunk = P::B % 2 ? P::B : P::B - 1;
-        if (P::HQ == 4 && chunk > 255) return hipErrorInvalidValue;
-        const u64 nunits = cnt / chunk;
-        if (nunits > 0xffffffffull) return hipErrorInvalidValue;
-        const u64 tail = cnt - nunits * chunk;  // < chunk <= B: one number per lane
+        u64 cnt = left < max_count ? left : max_count;
+        u64 chunk = 0, nunits = 0, tail = 0, grid = 0;
+        const u64 nw = P::WG / 64;
+        for (;;) {
+            // Chunk floor for fields too small to fill the chip: a lane's init
+            // costs about ten steps, but with idle CUs latency wins (b40 1e6:
+            // kernel 25 us at a floor of 32, 14 us at 4; scripts/small_fields.py).
+            const u64 min_chunk = probe_knob("NICE_FD2_MINCHUNK", 4);
+            // Whole rounds of workgroups, chunks <= the target (and <= B, the
+            // low-digit table's reach).
+            u64 rounds = (cnt + tchunk * lanes - 1) / (tchunk * lanes);
+            if (rounds < 1) rounds = 1;
+            chunk = (cnt + rounds * lanes - 1) / (rounds * lanes);
+            if (chunk < min_chunk) chunk = cnt < min_chunk ? cnt : min_chunk;
+            if (chunk < 1) chunk = 1;
+            // Odd chunks: lane l of a wave then sits at n mod B = r0 + chunk * l,
+            // so its low-digit entries fall on 32 distinct bank pairs per
+            // half-wave (B is a multiple of 32 for the LSD bases).  Without a
+            // low-digit table (b80) limb 0 of n^2 and n^3 is looked up in the
+            // pair table, and a chunk divisible by 16 puts a 16-lane group on
+            // ONE bank quad for those lookups (n^2 mod 16 equal on every lane):
+            // b80 1e9 at chunk 2544 took 11.8 ms, at 2545 9.3.
+            if (chunk > 1 && (P::LSD ? chunk % 2 == 0 : chunk % 16 == 0)) chunk++;
+            if (chunk > P::B) chunk = P::B % 2 ? P::B : P::B - 1;
+            if (P::HQ == 4 && chunk > 255) return hipErrorInvalidValue;
+            nunits = cnt / chunk;
+            tail = cnt - nunits * chunk;  // < chunk <= B: one number per lane
+            bool fits = nunits <= 0xffffffffull;
+            if constexpr (P::PERS) {
+                // one round of resident workgroups (fewer when the batches
+                // run out); the batch count stays in 32 bits and every
+                // workgroup's batches fit its waves' caps (u16 counters)
+                const u64 nb = (nunits + 63) / 64 + (tail + 63) / 64;
+                grid = std::min<u64>((u64)num_cus * per_cu, (nb + nw - 1) / nw);
+                fits = fits && nunits <= 0xffffffc0ull && (nb + grid - 1) / grid <= nw * (65535 / chunk);
+            } else {
+                grid = (nunits + P::WG - 1) / P::WG + (tail + P::WG - 1) / P::WG;
+            }
+            if (fits) break;
+            // Too much for one launch of this shape: split the segment (the
+            // finish rides on the last launch, so any split is exact).
+            if (cnt < 2) return hipErrorInvalidValue;
+            cnt /= 2;
+        }
         const u64 main_blocks = (nunits + P::WG - 1) / P::WG;  // one chunk per lane
-        const u64 tail_blocks = (tail + P::WG - 1) / P::WG;
         Fd2Args a{};
 #ifdef NICE_PROBES
         a.stamps = g_stamps;
@@ -1291,25 +1313,13 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         a.fin = left == cnt ? q.fin : FieldFinish{nullptr, nullptr};
 #ifdef NICE_PROBES
         {
-            const u64 v[6] = {P::PERS ? std::min<u64>((u64)num_cus * per_cu, ((nunits + 63) / 64 + (tail + 63) / 64 +
-                                                                            P::WG / 64 - 1) / (P::WG / 64))
-                                      : main_blocks + tail_blocks,
-                              (u64)P::WG, chunk, nunits, tail, (u64)per_cu};
+            const u64 v[6] = {grid, (u64)P::WG, chunk, nunits, tail, (u64)per_cu};
             for (int k = 0; k < 6; k++) g_last_launch[k] = v[k];
         }
 #endif
-        u64 grid = main_blocks + tail_blocks;
-        if constexpr (P::PERS) {
-            // one round of resident workgroups (fewer when the batches run out);
-            // a.nunits < 2^32 - 63 keeps the batch count in 32 bits
-            const u64 nb = (nunits + 63) / 64 + (tail + 63) / 64, nw = P::WG / 64;
-            grid = std::min<u64>((u64)num_cus * per_cu, (nb + nw - 1) / nw);
-            if (nunits > 0xffffffc0ull) return hipErrorInvalidValue;
-            // every workgroup's range fits its waves' caps (u16 counters)
-            if ((nb + grid - 1) / grid > nw * a.wave_cap) return hipErrorInvalidValue;
-        }
         hipLaunchKernelGGL(kern, dim3((u32)grid), dim3(P::WG), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (p.launches) ++*p.launches;
         add_u128(q.start_lo, q.start_hi, cnt);
         left -= cnt;
     }

@@ -40,6 +40,7 @@ struct DetailedLaunch {
     uint32_t hist_copies;        // fd2: copies the field's launches use (set by launch_detailed_fd2)
     NumOut out;
     FieldFinish fin;             // fd2 only; see FieldFinish
+    uint32_t *launches;          // if set, incremented per kernel launch enqueued
 };
 
 // Production FD kernel (fd2_detailed.hip): bases 40, 50, 80, in-range segments.

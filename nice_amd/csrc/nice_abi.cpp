@@ -164,12 +164,14 @@ struct Slot {
     uint64_t *d_fin = nullptr;    // device view of h_fin
     ListBuf det, nice;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_done = nullptr, nice_done = nullptr;
+    hipEvent_t nt0 = nullptr, nt1 = nullptr;  // niceonly field span on the GPU (adaptive floor)
     uint32_t *h_msd = nullptr;    // mapped: MSD counters at the end of a niceonly field
     uint32_t *h_nice = nullptr;   // mapped: niceonly list count
     uint32_t *d_msd_mapped = nullptr, *d_nice_mapped = nullptr;  // device views
     uint32_t *d_nice_done = nullptr;  // workgroups retired (niceonly in-kernel finish)
     bool dirty = true;            // state block not known to be zero
     uint64_t seq = 0;             // last detailed field's sequence number
+    uint32_t launches = 0;        // ... and its kernel launches (the finish kernel not counted)
     bool fin_seq = false;         // ... and whether its fd2 finish publishes it
     MsdBuf msd;
 };
@@ -213,6 +215,7 @@ struct Entry {
 // A submitted field, until its results have been handed to the caller.
 struct DetJob {
     bool active = false, collected = false;
+    bool waiting = false;          // a collect is waiting for it outside the context lock
     u128 s = 0, e = 0;
     uint32_t base = 0;
     std::vector<u128> bounds;      // per-device shard bounds
@@ -221,7 +224,12 @@ struct DetJob {
 };
 struct NiceJob {
     bool active = false, collected = false;
+    bool waiting = false;          // a collect is waiting for it outside the context lock
+    // the submitted field, kept so that collect can re-run it (list overflow)
+    u128 s = 0, e = 0;
     uint32_t base = 0;
+    nice_niceonly_opts opts{};
+    bool has_opts = false;
     bool on_device = false;
     bool empty = false;            // nothing enqueued (residue-empty base, no chunk dealt)
     std::vector<char> used;        // devices that ran part of the field
@@ -229,6 +237,7 @@ struct NiceJob {
     std::chrono::steady_clock::time_point t0;
     std::vector<Entry> all;
     bool adapt = false;            // host-MSD field on the adaptive floor: update it at collect
+    uint32_t reruns = 0;           // times the field was re-run with grown device lists
 };
 
 }  // namespace
@@ -352,6 +361,8 @@ int slot_init(Device &d, Slot &sl, const Slot *share) {
     HIPCHK(hipEventCreate(&sl.ev1));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.nice_done, hipEventDisableTiming));
+    HIPCHK(hipEventCreate(&sl.nt0));
+    HIPCHK(hipEventCreate(&sl.nt1));
     int rc = ensure_listbuf(d, sl.det, kInitialListCap, true);
     if (!rc) rc = ensure_listbuf(d, sl.nice, kNiceCap, false);
     return rc;
@@ -405,7 +416,7 @@ void device_free(Device &d) {
         if (sl.h_fin) (void)hipHostFree(sl.h_fin);
         if (sl.h_msd) (void)hipHostFree(sl.h_msd);
         if (sl.h_nice) (void)hipHostFree(sl.h_nice);
-        for (hipEvent_t ev : {sl.ev0, sl.ev1, sl.ev_done, sl.nice_done})
+        for (hipEvent_t ev : {sl.ev0, sl.ev1, sl.ev_done, sl.nice_done, sl.nt0, sl.nt1})
             if (ev) (void)hipEventDestroy(ev);
     }
     if (d.chk_n) (void)hipFree(d.chk_n);
@@ -476,6 +487,7 @@ int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *f
     p.cutoff = nice::near_miss_cutoff(base);
     p.hist = sl.d_state;
     p.out = nice::NumOut{sl.det.n, sl.det.u, sl.d_count, sl.det.cap};
+    p.launches = &sl.launches;
     *finished = false;
     auto launch = [&](u128 a, u128 b, bool fd) -> int {
         if (a >= b) return NICE_OK;
@@ -495,6 +507,7 @@ int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *f
             const bool fd2 = fd;
             hipError_t err = fd ? nice::launch_detailed_fd2(p, d.num_cus, sl.stream)
                                 : nice::launch_detailed_generic(p, d.num_cus, sl.stream);
+            if (!fd) sl.launches++;
             if (err != hipSuccess)
                 return fail(NICE_ERR_HIP, std::string("detailed launch: ") + hipGetErrorString(err));
             if (last) *finished = fd2 && p.fin.out_mapped;
@@ -543,14 +556,34 @@ int resolve_stats(Device &d) {
 // completion signal (which still follows: the last workgroup retires after
 // publishing).  The completion event is queried every 4096 polls, so a failed
 // launch or a finish that never publishes is reported, not spun on.
+// Polls spin for the first kSpinPolls (a small field ends within tens of
+// microseconds, and a sleeping waiter would add its wake-up latency), then
+// yield the core between polls.
+constexpr uint32_t kSpinPolls = 1u << 14;
+
+inline void backoff(uint32_t i) {
+    if (i < kSpinPolls) __builtin_ia32_pause();
+    else sched_yield();
+}
+
+// Wait for an event by polling it (see backoff).
+hipError_t sync_event(hipEvent_t ev) {
+    for (uint32_t i = 0;; i++) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q != hipErrorNotReady) return q;
+        backoff(i);
+    }
+}
+
 int wait_field(Slot &sl) {
     if (!sl.fin_seq || !spin_wait()) {
-        HIPCHK(hipEventSynchronize(done_event(sl)));
+        const hipError_t q = sync_event(done_event(sl));
+        if (q != hipSuccess) return fail(NICE_ERR_HIP, std::string("detailed field: ") + hipGetErrorString(q));
         return NICE_OK;
     }
     for (uint32_t i = 1;; i++) {
         if (__atomic_load_n(&sl.h_fin[130], __ATOMIC_ACQUIRE) == sl.seq) return NICE_OK;
-        if ((i & 4095) == 0) {
+        if ((i & 4095) == 0 || i > kSpinPolls) {
             const hipError_t q = hipEventQuery(done_event(sl));
             if (q == hipSuccess) {
                 if (__atomic_load_n(&sl.h_fin[130], __ATOMIC_ACQUIRE) == sl.seq) return NICE_OK;
@@ -558,7 +591,7 @@ int wait_field(Slot &sl) {
             }
             if (q != hipErrorNotReady) return fail(NICE_ERR_HIP, std::string("detailed field: ") + hipGetErrorString(q));
         }
-        __builtin_ia32_pause();
+        backoff(i);
     }
 }
 
@@ -571,6 +604,7 @@ int enqueue_detailed_shard(Device &d, Slot &sl, u128 s, u128 e, uint32_t base) {
         if (rc) return rc;
     }
     sl.seq++;
+    sl.launches = 0;
     // The state block is zeroed by the previous field's finish; a memset
     // only after an interrupted field (or the first one).
     if (sl.dirty) HIPCHK(hipMemsetAsync(sl.d_state, 0, kStateBytes, sl.stream));
@@ -632,7 +666,7 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
         sl.dirty = false;  // the epilogue zeroed the state block
         d.stats_slot = t;  // kernel_ms read on demand (resolve_stats)
         d.last.numbers = (uint64_t)(job.bounds[i + 1] - job.bounds[i]);
-        d.last.launches = 1;
+        d.last.launches = sl.launches;
         d.last.fd_kernel = nice::fd2_supported(base) ? 1u : 0u;
         uint32_t cnt = (uint32_t)sl.h_fin[129];
         if (cnt > sl.det.cap) {
@@ -645,6 +679,7 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
             if (rc) return rc;
             sl.dirty = false;
             d.stats_slot = t;
+            d.last.launches = sl.launches;
             cnt = (uint32_t)sl.h_fin[129];
             if (cnt > sl.det.cap) return fail(NICE_ERR_HIP, "near-miss list overflow after resize");
         }
@@ -847,7 +882,32 @@ int nice_detailed_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
 int nice_detailed_collect(nice_ctx *ctx, int ticket, uint64_t *hist, nice_number *out, size_t cap,
                           size_t *n_out) {
     if (!ctx || !hist) return fail(NICE_ERR_INVALID, "null argument");
-    std::lock_guard<std::mutex> lock(ctx->mu);
+    std::unique_lock<std::mutex> lock(ctx->mu);
+    if (ticket < 0 || ticket >= kSlots || !ctx->det[ticket].active)
+        return fail(NICE_ERR_INVALID, "no detailed field in flight under this ticket");
+    DetJob &job = ctx->det[ticket];
+    if (job.waiting) return fail(NICE_ERR_INVALID, "another thread is collecting this detailed field");
+    if (!job.collected) {
+        // Wait for every device's shard to publish WITHOUT the context lock,
+        // so other threads can submit and collect other fields meanwhile (the
+        // slot stays reserved: the job is active).  The gather below then
+        // finds them finished.
+        job.waiting = true;
+        lock.unlock();
+        int rc = NICE_OK;
+        for (size_t i = 0; i < ctx->devs.size() && !rc; i++) {
+            if (job.bounds[i] >= job.bounds[i + 1]) continue;
+            const hipError_t err = hipSetDevice(ctx->devs[i].id);
+            rc = err != hipSuccess ? fail(NICE_ERR_HIP, hipGetErrorString(err)) : wait_field(ctx->devs[i].slot[ticket]);
+        }
+        lock.lock();
+        job.waiting = false;
+        if (rc) {
+            job.active = false;
+            for (auto &d : ctx->devs) d.slot[ticket].dirty = true;
+            return rc;
+        }
+    }
     return detailed_collect(ctx, ticket, hist, out, cap, n_out);
 }
 
@@ -1113,23 +1173,36 @@ int nice_adaptive_floor(double *floor, uint32_t *warmup) {
     return NICE_OK;
 }
 
-int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, uint64_t end_lo,
-                         uint64_t end_hi, uint32_t base, const nice_niceonly_opts *opts, int *ticket) {
-    using clock = std::chrono::steady_clock;
-    const auto t0 = clock::now();
-    if (!ctx || !ticket) return fail(NICE_ERR_INVALID, "null argument");
-    if (base < 3 || base > 128) return fail(NICE_ERR_INVALID, "base must be in 3..=128");
-    const u128 s = mk(start_lo, start_hi), e = mk(end_lo, end_hi);
-    if (s >= e)
-        return fail(NICE_ERR_INVALID, "Range has invalid bounds, range_start must be < range_end");
-    nice_niceonly_stats st{};
-    const bool adaptive = opts && opts->msd_floor == NICE_MSD_FLOOR_ADAPTIVE;
+}  // extern "C"
+
+namespace {
+
+// The floor a niceonly field's MSD recursion uses (resolved once per field:
+// a re-run of the field keeps it).
+uint64_t resolve_floor(const nice_niceonly_opts *opts) {
     uint64_t floor_size = opts && opts->msd_floor ? opts->msd_floor : env_msd_floor();
-    if (adaptive) {
+    if (opts && opts->msd_floor == NICE_MSD_FLOOR_ADAPTIVE) {
         std::lock_guard<std::mutex> g(g_af_mu);
         floor_size = (uint64_t)adaptive_floor().floor;  // gpu_msd_floor(), client_process_gpu.rs:559-561
     }
-    if (!floor_size) floor_size = 250;
+    return floor_size ? floor_size : 250;
+}
+
+// Enqueue niceonly field `job` (bounds, base, options and floor already set)
+// into slot t of the context's devices.  Called under ctx->mu by submit, and
+// again by collect when a device's nice list overflowed and was grown: the
+// whole field re-runs (the reference CPU path returns a list of any length,
+// client_process.rs:439-465; its GPU path bails at 2^16,
+// client_process_gpu.rs:777-782).
+int niceonly_enqueue(nice_ctx *ctx, int t, NiceJob &job) {
+    using clock = std::chrono::steady_clock;
+    const auto t0 = clock::now();
+    const u128 s = job.s, e = job.e;
+    const uint32_t base = job.base;
+    const nice_niceonly_opts *opts = job.has_opts ? &job.opts : nullptr;
+    nice_niceonly_stats st{};
+    const bool adaptive = opts && opts->msd_floor == NICE_MSD_FLOOR_ADAPTIVE;
+    const uint64_t floor_size = job.st.msd_floor;
     st.msd_floor = floor_size;
     const uint32_t k = opts && opts->stride_k ? opts->stride_k : 2;
     int threads = opts && opts->threads > 0 ? opts->threads : (int)std::thread::hardware_concurrency();
@@ -1149,21 +1222,12 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
         ce = std::min(e, cs + chunk);
     };
 
-    std::lock_guard<std::mutex> lock(ctx->mu);
-    const int t = free_slot(ctx->nice, ctx->nice_next);
-    if (t < 0)
-        return fail(NICE_ERR_INVALID, "three niceonly fields already in flight on this context; collect one first");
-    NiceJob &job = ctx->nice[t];
-    job = NiceJob{};
-    job.base = base;
-    job.t0 = t0;
     job.used.assign(ctx->devs.size(), 0);
-    auto finish_submit = [&]() {
-        job.active = true;
-        ctx->nice_next = (t + 1) % slots_used();
-        *ticket = t;
-        return NICE_OK;
-    };
+    job.all.clear();
+    job.empty = false;
+    job.collected = false;
+    job.st = st;
+    auto finish_submit = [&]() { return NICE_OK; };
     if (nice::residue_filter(base).empty() || mine == 0) {  // client_process_gpu.rs:525-531
         job.empty = true;
         return finish_submit();
@@ -1384,6 +1448,9 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
     } else {
         for (auto &d : ctx->devs) {
             HIPCHK(hipSetDevice(d.id));
+            // the adaptive floor's GPU-tail clock starts with the field (the
+            // stream reaches this event as soon as it is idle)
+            if (job.adapt) HIPCHK(hipEventRecord(d.slot[t].nt0, d.slot[t].nstream));
             HIPCHK(hipMemsetAsync(d.slot[t].d_nice_count, 0, 4, d.slot[t].nstream));
             d.slot[t].msd.dirty = true;  // the nice count is left set
         }
@@ -1503,6 +1570,7 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
             HIPCHK(hipMemcpyAsync(d.slot[t].h_nice, d.slot[t].d_nice_count, 4, hipMemcpyDeviceToHost,
                                   d.slot[t].nstream));
             HIPCHK(hipEventRecord(d.slot[t].nice_done, d.slot[t].nstream));
+            if (job.adapt) HIPCHK(hipEventRecord(d.slot[t].nt1, d.slot[t].nstream));
         }
     }
     if (rc) return rc;
@@ -1510,56 +1578,136 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
     return finish_submit();
 }
 
+// Read a finished niceonly field's results from the devices (its events have
+// completed).  *grow receives, per device, the list length when it exceeded
+// that device's list capacity (0 otherwise).
+int niceonly_gather(nice_ctx *ctx, NiceJob &job, int t, std::vector<uint32_t> &grow) {
+    grow.assign(ctx->devs.size(), 0);
+    bool over = false;
+    for (size_t i = 0; i < ctx->devs.size(); i++) {
+        Device &d = ctx->devs[i];
+        Slot &sl = d.slot[t];
+        if (!job.used[i]) continue;  // no batch of this field ran there
+        HIPCHK(hipSetDevice(d.id));
+        HIPCHK(hipEventSynchronize(sl.nice_done));
+        if (job.on_device) {
+            const uint32_t *c = sl.h_msd;
+            sl.msd.dirty = false;  // the epilogue re-zeroed counters and count
+#ifdef NICE_PROBES
+            if (getenv("NICE_MSD_TRACE")) {  // level sizes of the last batch (diagnostics)
+                fprintf(stderr, "msd levels:");
+                for (int lv = 0; lv < 24; lv++) fprintf(stderr, " %u", c[lv]);
+                fprintf(stderr, " | ranges %u\n", c[26]);
+            }
+#endif
+            if (c[25])
+                return fail(NICE_ERR_MSD_OVERFLOW, "device MSD queue overflow (msd_floor too small "
+                                               "for chunk_size); use msd_where = host");
+            uint64_t cand, nums;
+            std::memcpy(&cand, c + 28, 8);
+            std::memcpy(&nums, c + 30, 8);
+            job.st.ranges += c[26];
+            job.st.candidates += cand;
+            job.st.range_numbers += nums;
+            job.st.square_ok += c[27];
+        }
+        const uint32_t cnt = *sl.h_nice;
+        if (cnt > sl.nice.cap) {
+            // more nice numbers than the device list holds (the kernels count
+            // every hit, store those below the capacity): grow and re-run
+            grow[i] = cnt;
+            over = true;
+            continue;
+        }
+        if (cnt && !over) {
+            std::vector<uint64_t> nbuf((size_t)cnt * 2);
+            HIPCHK(hipMemcpy(nbuf.data(), sl.nice.n, (size_t)cnt * 16, hipMemcpyDeviceToHost));
+            for (uint32_t q = 0; q < cnt; q++) job.all.push_back({mk(nbuf[2 * q], nbuf[2 * q + 1]), job.base});
+        }
+    }
+    return NICE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, uint64_t end_lo,
+                         uint64_t end_hi, uint32_t base, const nice_niceonly_opts *opts, int *ticket) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!ctx || !ticket) return fail(NICE_ERR_INVALID, "null argument");
+    if (base < 3 || base > 128) return fail(NICE_ERR_INVALID, "base must be in 3..=128");
+    const u128 s = mk(start_lo, start_hi), e = mk(end_lo, end_hi);
+    if (s >= e)
+        return fail(NICE_ERR_INVALID, "Range has invalid bounds, range_start must be < range_end");
+    if (opts && opts->deal_offset >= (opts->deal_stride ? opts->deal_stride : 1u))
+        return fail(NICE_ERR_INVALID, "deal_offset must be < deal_stride");
+    const uint64_t floor_size = resolve_floor(opts);
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    const int t = free_slot(ctx->nice, ctx->nice_next);
+    if (t < 0)
+        return fail(NICE_ERR_INVALID, "three niceonly fields already in flight on this context; collect one first");
+    NiceJob &job = ctx->nice[t];
+    job = NiceJob{};
+    job.s = s;
+    job.e = e;
+    job.base = base;
+    job.has_opts = opts != nullptr;
+    if (opts) job.opts = *opts;
+    job.st.msd_floor = floor_size;
+    job.t0 = t0;
+    const int rc = niceonly_enqueue(ctx, t, job);
+    if (rc) return rc;
+    job.active = true;
+    ctx->nice_next = (t + 1) % slots_used();
+    *ticket = t;
+    return NICE_OK;
+}
+
 int nice_niceonly_collect(nice_ctx *ctx, int t, nice_number *out, size_t cap, size_t *n_out,
                           nice_niceonly_stats *stats) {
     if (!ctx) return fail(NICE_ERR_INVALID, "null ctx");
-    std::lock_guard<std::mutex> lock(ctx->mu);
+    std::unique_lock<std::mutex> lock(ctx->mu);
     if (t < 0 || t >= kSlots || !ctx->nice[t].active)
         return fail(NICE_ERR_INVALID, "no niceonly field in flight under this ticket");
     NiceJob &job = ctx->nice[t];
+    if (job.waiting) return fail(NICE_ERR_INVALID, "another thread is collecting this niceonly field");
     if (!job.collected) {
-        auto gather = [&]() -> int {
-            for (size_t i = 0; i < ctx->devs.size(); i++) {
-                Device &d = ctx->devs[i];
-                Slot &sl = d.slot[t];
-                if (!job.used[i]) continue;  // no batch of this field ran there
-                HIPCHK(hipSetDevice(d.id));
-                HIPCHK(hipEventSynchronize(sl.nice_done));
-                if (job.on_device && job.used[i]) {
-                    const uint32_t *c = sl.h_msd;
-                    sl.msd.dirty = false;  // the epilogue re-zeroed counters and count
-#ifdef NICE_PROBES
-                    if (getenv("NICE_MSD_TRACE")) {  // level sizes of the last batch (diagnostics)
-                        fprintf(stderr, "msd levels:");
-                        for (int lv = 0; lv < 24; lv++) fprintf(stderr, " %u", c[lv]);
-                        fprintf(stderr, " | ranges %u\n", c[26]);
-                    }
-#endif
-                    if (c[25])
-                        return fail(NICE_ERR_MSD_OVERFLOW, "device MSD queue overflow (msd_floor too small "
-                                                       "for chunk_size); use msd_where = host");
-                    uint64_t cand, nums;
-                    std::memcpy(&cand, c + 28, 8);
-                    std::memcpy(&nums, c + 30, 8);
-                    job.st.ranges += c[26];
-                    job.st.candidates += cand;
-                    job.st.range_numbers += nums;
-                    job.st.square_ok += c[27];
-                }
-                const uint32_t cnt = *sl.h_nice;
-                if (cnt > sl.nice.cap)
-                    return fail(NICE_ERR_HIP, "niceonly output buffer overflow: " + std::to_string(cnt) +
-                                                  " (this strongly suggests a kernel bug)");
-                if (cnt) {
-                    std::vector<uint64_t> nbuf((size_t)cnt * 2);
-                    HIPCHK(hipMemcpy(nbuf.data(), sl.nice.n, (size_t)cnt * 16, hipMemcpyDeviceToHost));
-                    for (uint32_t q = 0; q < cnt; q++)
-                        job.all.push_back({mk(nbuf[2 * q], nbuf[2 * q + 1]), job.base});
-                }
+        int rc = NICE_OK;
+        if (!job.empty) {
+            // Wait for the devices WITHOUT the context lock, so other threads
+            // can submit and collect other fields meanwhile (the slot stays
+            // reserved: the job is active).
+            job.waiting = true;
+            lock.unlock();
+            for (size_t i = 0; i < ctx->devs.size() && !rc; i++) {
+                if (!job.used[i]) continue;
+                Slot &sl = ctx->devs[i].slot[t];
+                hipError_t err = hipSetDevice(ctx->devs[i].id);
+                if (err == hipSuccess) err = sync_event(sl.nice_done);
+                if (err != hipSuccess) rc = fail(NICE_ERR_HIP, std::string("niceonly field: ") + hipGetErrorString(err));
             }
-            return NICE_OK;
-        };
-        const int rc = job.empty ? NICE_OK : gather();
+            lock.lock();
+            job.waiting = false;
+        }
+        std::vector<uint32_t> grow;
+        if (!rc && !job.empty) rc = niceonly_gather(ctx, job, t, grow);
+        for (uint32_t attempt = 0; !rc && !job.empty; attempt++) {
+            bool over = false;
+            for (uint32_t g : grow) over |= g != 0;
+            if (!over) break;
+            if (attempt) {
+                rc = fail(NICE_ERR_HIP, "niceonly list overflowed again after growing it to the field's count");
+                break;
+            }
+            // Grow the overflowing devices' lists to the counts the kernels
+            // reported and re-run the field (under the lock: rare).
+            for (size_t i = 0; i < ctx->devs.size() && !rc; i++)
+                if (grow[i]) rc = ensure_listbuf(ctx->devs[i], ctx->devs[i].slot[t].nice, (grow[i] + 4095u) & ~4095u, false);
+            if (!rc) rc = niceonly_enqueue(ctx, t, job);
+            if (!rc) job.reruns++;
+            if (!rc) rc = niceonly_gather(ctx, job, t, grow);
+        }
         if (rc) {
             job.active = false;
             return rc;
@@ -1568,13 +1716,26 @@ int nice_niceonly_collect(nice_ctx *ctx, int t, nice_number *out, size_t cap, si
             std::chrono::duration<double>(std::chrono::steady_clock::now() - job.t0).count();
         job.collected = true;
         if (job.adapt) {  // update_msd_floor (client_process_gpu.rs:551, 563-568, 130-157)
+            // The GPU tail ends when the field's last device work does (its
+            // end event), not when the caller gets round to collecting: the
+            // reference times both phases inside one call (:541-551).
+            double gpu_end = 0;
+            for (size_t i = 0; i < ctx->devs.size(); i++) {
+                if (!job.used[i]) continue;
+                Slot &sl = ctx->devs[i].slot[t];
+                float ms = 0;
+                if (hipSetDevice(ctx->devs[i].id) == hipSuccess &&
+                    hipEventElapsedTime(&ms, sl.nt0, sl.nt1) == hipSuccess)
+                    gpu_end = std::max(gpu_end, ms * 1e-3);
+            }
+            const double total = std::max(job.st.msd_seconds, gpu_end);
             std::lock_guard<std::mutex> g(g_af_mu);
             AdaptiveFloor &af = adaptive_floor();
             if (af.warmup == kAdaptPinned) {
             } else if (af.warmup > 0) {
                 af.warmup--;
             } else {
-                af.floor = nice_adaptive_floor_step(af.floor, job.st.msd_seconds, job.st.total_seconds);
+                af.floor = nice_adaptive_floor_step(af.floor, job.st.msd_seconds, total);
             }
         }
     }

@@ -12,10 +12,21 @@ time).  Derived:
   valu_lane_ops_per_n SQ_INSTS_VALU x 64 / numbers per dispatch
   lds_instr_per_n     SQ_INSTS_LDS x 64 / numbers
   lds_conflict_frac   SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
+  kernel_cycles       GRBM_GUI_ACTIVE / XCDs (the CSV sums the 8 XCD instances;
+                      VALUBusy's own expression takes their max)
+  lds_busy            SQ_LDS_IDX_ACTIVE / CUs / kernel_cycles: the share of the
+                      kernel's cycles the CU's one LDS pipe is busy (the counter
+                      aggregates the SIMDs of each SE)
+  lds_cycles_per_instr SQ_LDS_IDX_ACTIVE / SQ_INSTS_LDS (LDS cycles per wave64
+                      LDS instruction; 4 is a conflict-free ds_read_b128)
   traffic_bytes       HBM bytes: FETCH_SIZE x 2 + WRITE_SIZE (KB -> B), separate passes
+The output records the sha256 (16 hex digits) of the library profiled
+(--lib, default nice_amd/libnice_hip.so): bench.py reports these figures only
+while it loads that same library.
 """
 import argparse
 import collections
+import hashlib
 import csv
 import glob
 import json
@@ -27,6 +38,10 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--numbers", type=float, required=True, help="numbers per fd2 dispatch")
 ap.add_argument("--kernel", default=KERNEL)
 ap.add_argument("--out", required=True)
+ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                           "nice_amd", "libnice_hip.so"))
+ap.add_argument("--cus", type=int, default=256)
+ap.add_argument("--xcds", type=int, default=8)
 ap.add_argument("dirs", nargs="+")
 a = ap.parse_args()
 
@@ -46,7 +61,9 @@ for d in a.dirs:
 if not vals:
     raise SystemExit(f"no {a.kernel} rows under {a.dirs}")
 mean = {c: sum(v) / len(v) for c, v in vals.items()}
-out = {"kernel": sorted(names), "numbers_per_dispatch": a.numbers,
+with open(a.lib, "rb") as fh:
+    sha16 = hashlib.sha256(fh.read()).hexdigest()[:16]
+out = {"kernel": sorted(names), "numbers_per_dispatch": a.numbers, "lib_sha16": sha16,
        "dispatches": {c: len(v) for c, v in vals.items()},
        "per_dispatch": {c: round(v, 4) for c, v in sorted(mean.items())},
        "files": [os.path.relpath(f) for f in files]}
@@ -59,6 +76,12 @@ if "SQ_INSTS_LDS" in mean:
     der["lds_instr_per_n"] = mean["SQ_INSTS_LDS"] * 64 / a.numbers
 if "SQ_LDS_BANK_CONFLICT" in mean and mean.get("SQ_LDS_IDX_ACTIVE"):
     der["lds_conflict_frac"] = mean["SQ_LDS_BANK_CONFLICT"] / mean["SQ_LDS_IDX_ACTIVE"]
+if "GRBM_GUI_ACTIVE" in mean:
+    der["kernel_cycles"] = mean["GRBM_GUI_ACTIVE"] / a.xcds
+    if "SQ_LDS_IDX_ACTIVE" in mean:
+        der["lds_busy"] = mean["SQ_LDS_IDX_ACTIVE"] / a.cus / der["kernel_cycles"]
+if "SQ_LDS_IDX_ACTIVE" in mean and mean.get("SQ_INSTS_LDS"):
+    der["lds_cycles_per_instr"] = mean["SQ_LDS_IDX_ACTIVE"] / mean["SQ_INSTS_LDS"]
 if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     # HBM bytes per dispatch: FETCH_SIZE doubled (gfx950 tallies 128-B requests
     # at 64 B, MI355X_MICROARCH.md), WRITE_SIZE as read; both in KB

@@ -377,3 +377,18 @@ def test_field_pipeline_single_process():
         assert [(n.number, n.num_uniques) for n in det.nice_numbers] == w.nice_numbers
         assert [n.number for n in nic.nice_numbers] == \
             [n for n, _ in O.process_field_niceonly_mt(f.range_start, f.range_end, 10, 2)[0].nice_numbers]
+
+
+def test_bench_refuses_a_world_size_other_than_gpus():
+    """bench.py under a launcher whose WORLD_SIZE differs from --gpus exits
+    non-zero before touching a device (a run that would time another number
+    of GPUs than it reports); --gpus 0 likewise."""
+    import subprocess
+    import sys
+    bench = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
+    for world, gpus in (("3", "2"), ("1", "8"), ("2", "1")):
+        out = subprocess.run([sys.executable, bench, "--gpus", gpus], capture_output=True, text=True,
+                             timeout=60, env=dict(os.environ, WORLD_SIZE=world, RANK="0", LOCAL_RANK="0"))
+        assert out.returncode == 2 and "WORLD_SIZE" in out.stderr and out.stdout == ""
+    out = subprocess.run([sys.executable, bench, "--gpus", "0"], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 2 and out.stdout == ""

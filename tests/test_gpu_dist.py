@@ -87,21 +87,27 @@ def test_two_rank_strong_pipeline_on_gpu():
     assert res[0]["massive"][2] == [] and res[1]["massive"][2] == []
 
 
-def test_bench_two_ranks_strong_scaling_branch():
-    """bench.py's N > 1 path end to end, as the driver's scaling run launches it
-    (torch.distributed.run, one process per rank), with gloo collectives so two
-    ranks can share the one GPU of the test box: the line carries the
-    strong-scaling fields (t1_ms_per_step, strong_efficiency, parallelism
-    strong2) and every field of the timed region came back whole and was
-    checked (fields_checked == steps)."""
+@pytest.mark.parametrize("launcher", ["torchrun", "self"])
+def test_bench_two_ranks_strong_scaling_branch(launcher):
+    """bench.py's N > 1 path end to end, with gloo collectives so two ranks can
+    share the one GPU of the test box -- as the driver's scaling run launches
+    it (torch.distributed.run, one process per rank), and as a bare
+    `bench.py --gpus 2`, which starts that launcher itself as a child process:
+    the line carries n_gpus 2 and the strong-scaling fields (t1_ms_per_step,
+    strong_efficiency, parallelism strong2) and every field of the timed
+    region came back whole and was checked (fields_checked == steps)."""
     import subprocess
     import sys
-    port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "6", "--warmup", "2", "--no-cpu-baseline", "--dist-backend", "gloo"]
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
+            "--no-cpu-baseline", "--dist-backend", "gloo"]
+    if launcher == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
+    else:
+        cmd = [sys.executable] + args
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT,
-                         env=dict(os.environ, OMP_NUM_THREADS="4"))
+                         env=dict(env, OMP_NUM_THREADS="4"))
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout  # rank 0 prints the one line

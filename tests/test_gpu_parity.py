@@ -442,23 +442,139 @@ def test_big_field_kernel_equals_small_field_kernel(ctx, base):
 
 @pytest.mark.parametrize("base", [42, 45, 49, 55, 58, 59, 64, 65, 67, 68])
 def test_persistent_grid_equals_rounds(ctx, base):
-    """Bases whose big-field kernel holds one workgroup per CU run fields of
-    >= 2 rounds on the persistent grid (waves pull strided 64-unit batches;
-    1024-thread workgroups); 1e8 windows (< 2 rounds) run in rounds of
-    workgroups (b42..50 and b59..64 at 512 threads).  A 1e9 field must
-    equal the sum of its ten 1e8 windows, and every near-miss recomputes by
-    the oracle.  (b52-54 and b80 1e9 are pinned to oracle fixtures in
+    """Bases whose big-field kernel holds one workgroup per CU run segments of
+    >= 2 rounds (2 x TCHUNK x resident lanes: 4.2e7 numbers at TCHUNK 80,
+    8.4e7 at 160, 1.26e8 at 240 on 256 CUs) on the persistent grid (waves
+    pull strided 64-unit batches; 1024-thread workgroups).  2.5e7 windows
+    are below every base's threshold, so they run in rounds of workgroups
+    (b42..50 and b59..64 at 512 threads).  A 1e9 field must equal the sum of
+    its forty 2.5e7 windows, and every near-miss recomputes by the oracle.
+    (b52-54 and b80 1e9 are pinned to oracle fixtures in
     test_fd_bases_whole_fields_1e9.)"""
     r0, r1 = O.base_range(base)
     s = r0 + (r1 - r0) // 3
     h, l = ctx.detailed_raw(s, s + 10 ** 9, base)
+    w = 25 * 10 ** 6
     hs, ls = [0] * len(h), []
-    for k in range(10):
-        hk, lk = ctx.detailed_raw(s + k * 10 ** 8, s + (k + 1) * 10 ** 8, base)
+    for k in range(40):
+        hk, lk = ctx.detailed_raw(s + k * w, s + (k + 1) * w, base)
         hs = [x + y for x, y in zip(hs, hk)]
         ls += lk
     assert h == hs and l == ls and sum(h) == 10 ** 9
     assert all(O.num_unique_digits(n, base) == u for n, u in l)
+
+
+@pytest.mark.parametrize("base,size", [(40, 32 * 10 ** 9), (80, 16 * 10 ** 9)])
+def test_detailed_field_longer_than_one_launch(ctx, base, size):
+    """launch_cfg (fd2_kernel.hpp) splits a segment into launches of at most
+    60 000 numbers per resident lane: 3.1e10 at b40 (two 1024-thread
+    workgroups per CU), 1.6e10 at b80 (one, persistent grid); the field's
+    finish rides on its last launch.  The reference batches any field size
+    (client_process_gpu.rs:832-856).  A field above one launch must report
+    more than one launch, hold exactly its size in the histogram, equal the
+    sum of two halves that each fit one launch, and every near-miss must
+    recompute by the oracle."""
+    r0, r1 = O.base_range(base)
+    s = r0 + (r1 - r0) // 5
+    h, l = ctx.detailed_raw(s, s + size, base)
+    assert ctx.kernel_stats().launches >= 2
+    assert sum(h) == size
+    m = s + size // 2 + 12_345
+    h1, l1 = ctx.detailed_raw(s, m, base)
+    assert ctx.kernel_stats().launches == 1
+    h2, l2 = ctx.detailed_raw(m, s + size, base)
+    assert [a + b for a, b in zip(h1, h2)] == h and l1 + l2 == l
+    assert sum(h[O.near_miss_cutoff(base) + 1:]) == len(l)
+    assert all(O.num_unique_digits(n, base) == u for n, u in l)
+
+
+@pytest.mark.parametrize("where", MSD_WHERE)
+@pytest.mark.parametrize("chunk", [0, 10 ** 8])
+def test_niceonly_list_longer_than_device_capacity(ctx, where, chunk):
+    """b100 [1, 1e7) lies below b100's valid range, where get_is_nice lists
+    every n whose n^2 and n^3 digits are merely distinct
+    (client_process.rs:222-253): 70 636 numbers on the client's 1e6 chunk
+    grid, 72 207 as ONE chunk (the CPU API's whole-range call,
+    client_process.rs:439-465; Filter C makes the two differ).  Both exceed
+    the device list's initial 2^16 entries, so the library grows the list
+    to the count the kernels report and re-runs the field.  Nice list,
+    candidates and MSD ranges against the oracle (cap 2^22), for both MSD
+    placements; then the same field through submit / collect with a caller
+    list too small (NICE_ERR_CAPACITY with the true length, results kept for
+    the retry)."""
+    res, cands, ranges, _ = O.process_field_niceonly_sq(1, 10 ** 7, 100, 8, chunk, 0, cap=1 << 22)
+    want = [n for n, _ in res.nice_numbers]
+    assert len(want) == (72_207 if chunk else 70_636)
+    lst, st = ctx.niceonly_raw(1, 10 ** 7, 100, chunk_size=chunk, msd_where=where)
+    assert lst == want
+    assert (st.candidates, st.ranges) == (cands, ranges)
+    lib = N._lib.lib()
+    ct = N._lib.ctypes
+    t = ctx.niceonly_submit(1, 10 ** 7, 100, chunk_size=chunk, msd_where=where)
+    out = (N._lib.nice_number * 16)()
+    n = ct.c_size_t()
+    st2 = N._lib.nice_niceonly_stats()
+    assert lib.nice_niceonly_collect(ctx._h, t, out, 16, n, st2) == N._lib.NICE_ERR_CAPACITY
+    assert n.value == len(want)
+    got, st3 = ctx.niceonly_collect(t, cap=n.value)
+    assert got == want and st3.candidates == cands
+
+
+def test_collect_waits_without_holding_the_context(ctx):
+    """A collect waits for its field outside the context lock: while thread
+    A collects a long b80 field, thread B submits (and collects) a detailed
+    and a niceonly field on the same context -- the pipelined loop of the
+    reference client (client/src/main.rs:411-562) with one thread per stage.
+    B's submits must return before A's collect does, and every result must
+    equal the synchronous call's.  Raw ABI calls with per-thread buffers."""
+    import threading
+    import time
+    lib = N._lib.lib()
+    ct = N._lib.ctypes
+    s40, s80 = O.base_range(40)[0], O.base_range(80)[0]
+    big = (s80, s80 + 5 * 10 ** 9)  # ~35 ms
+    small = (s40 + 7 * 10 ** 6, s40 + 8 * 10 ** 6)
+    want_big = ctx.detailed_raw(*big, 80)
+    want_small = ctx.detailed_raw(*small, 40)
+    want_nice = ctx.niceonly_raw(*small, 40)[0]
+
+    def submit_det(a, b, base):
+        t = ct.c_int()
+        assert lib.nice_detailed_submit(ctx._h, *N.api._split(a), *N.api._split(b), base, t) == 0
+        return t.value
+
+    def collect_det(t, base):
+        hist = (ct.c_uint64 * (base + 1))()
+        out = (N._lib.nice_number * 4096)()
+        n = ct.c_size_t()
+        assert lib.nice_detailed_collect(ctx._h, t, hist, out, 4096, n) == 0, lib.nice_last_error()
+        return list(hist), [(out[i].number_lo | (out[i].number_hi << 64), out[i].num_uniques)
+                            for i in range(n.value)]
+
+    res = {}
+    t_big = submit_det(*big, 80)
+
+    def a_thread():
+        res["big"] = collect_det(t_big, 80)
+        res["big_done"] = time.perf_counter()
+
+    th = threading.Thread(target=a_thread)
+    th.start()
+    time.sleep(0.003)  # A is inside its collect
+    t_small = submit_det(*small, 40)
+    tn = ct.c_int()
+    opts = N.GpuContext._nice_opts()
+    assert lib.nice_niceonly_submit(ctx._h, *N.api._split(small[0]), *N.api._split(small[1]), 40,
+                                    opts, tn) == 0
+    submitted = time.perf_counter()
+    got_small = collect_det(t_small, 40)
+    out = (N._lib.nice_number * 16)()
+    n = ct.c_size_t()
+    assert lib.nice_niceonly_collect(ctx._h, tn.value, out, 16, n, None) == 0
+    th.join()
+    assert submitted < res["big_done"], "submit waited for the other thread's collect"
+    assert res["big"] == want_big and got_small == want_small
+    assert [out[i].number_lo | (out[i].number_hi << 64) for i in range(n.value)] == want_nice
 
 
 def test_multi_device_context_sharding():
