@@ -11,7 +11,9 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnice_hip.so")
+# NICE_LIB_PATH: a CPU-only sanitizer build of the same sources
+# (make -C nice_amd sanitize; scripts/sanitize.sh)
+LIB_PATH = os.environ.get("NICE_LIB_PATH") or os.path.join(_HERE, "libnice_hip.so")
 
 NICE_OK = 0
 NICE_ERR_INVALID = 1

@@ -173,10 +173,19 @@ constexpr int valu_limbs(int base) {
 // LDS bytes / waves per SIMD of a base's kernel at a workgroup size (the
 // formulas of Cfg, evaluated without instantiating it).
 constexpr int lds_bytes(int base, int wg) {
-    const int mw = (base + 31) / 32, es = mw == 1 ? 4 : (mw == 2 ? 8 : 16), b2 = base * base;
+    const int mw = (base + 31) / 32, b2 = base * base;
+    const bool split = mw == 3 && (valu_limbs(base) & 512) != 0;
+    const int es = mw == 1 ? 4 : (mw == 2 || split ? 8 : 16);
     int t = 0;
     while ((1 << t) < b2) t++;
     const int ebt = es * ((1 << t) - b2);
+    if (split) {  // [OUTL | X2 | X1 | window rows] (Cfg::SPLIT)
+        const int a = (4 * (base + 1) + 15) / 16 * 16, h = (ebt / 2 + 15) / 16 * 16;
+        const int t2 = a > h ? a : h;
+        const int tb0 = (t2 + 4 * b2 + 15) / 16 * 16, tbe = (ebt + 15) / 16 * 16;
+        const int tb = tb0 > tbe ? tb0 : tbe;
+        return (tb + b2 * es + 15) / 16 * 16 + window_w(base) * (wg / 2) * 4;
+    }
     const int tb0 = (window_w(base) * (wg / 2) * 4 + 4 * (base + 1) + 15) / 16 * 16;
     const int tb = tb0 >= ebt ? tb0 : (ebt + 15) / 16 * 16;
     const int db = base - 32;
@@ -236,14 +245,16 @@ struct Cfg {
     static constexpr int T = log2ceil(B);
     static constexpr u32 BT = (1u << T) - B;
     static constexpr int MW = (BASE + 31) / 32;
-    // VD & 512 (three mask words, b65..68 / b80; probe A/B only): the 80-bit
-    // digit-pair masks SPLIT into an 8-byte table of the digits 0..63
-    // (ds_read_b64) and a u16 table of the digits 64.. (ds_read_u16), both at
-    // an 8-byte stride so one stored limb addresses both through two immediate
-    // offsets.  On uniformly random indices b64 + u16 costs 5.9-6.8 LDS cycles
-    // per wave-lookup against 10.5 for one b128 (scripts/ubench/lds_lookup.hip),
-    // but in the kernel it is 26 % slower on b80 1e9 (9.22 vs 7.31 ms,
-    // profiles/r03/lg_sweep.log): production keeps the 16-byte entries.
+    // VD & 512 (three mask words, b65..68 / b80): the digit-pair masks SPLIT
+    // into X1, 8-byte entries of the digits 0..63 (ds_read_b64), and X2, 4-byte
+    // entries of the digits 64.. (ds_read_b32), each table at its own entry
+    // size, so both spread a lane group over all 64 banks: the stored limb
+    // (scaled by 8) addresses X1 directly and X2 after one shift.  On the
+    // kernel's own b80 index pattern b64 + b32 costs 3.9 LDS cycles per
+    // wave-lookup against 11.4 for one b128 of a 16-byte entry
+    // (scripts/ubench/lds_trace.hip, profiles/r04/lds_trace.log).  (Round 3's
+    // split kept X2 at an 8-byte stride, which puts a 32-lane group on half
+    // the banks: 26 % slower than the b128 layout in the kernel.)
     static constexpr bool SPLIT = MW == 3 && (VD_ & 512) != 0;
     static constexpr int ES = MW == 1 ? 4 : (MW == 2 || SPLIT ? 8 : 16);  // table entry stride (bytes)
     static constexpr int SH = T + ilog2(ES);                     // carry bit of a scaled limb
@@ -258,24 +269,23 @@ struct Cfg {
     static constexpr int W = window_w(BASE);
     static constexpr int W0 = window_w0(BASE);
     // Window counters: HQ per dword (u16 halves shared by threads t and
-    // t + WG/2; SPLIT: u8 quarters, t + k WG/4 -- a lane counts at most one
-    // chunk of <= TCHUNK <= 255 numbers per launch).
-    static constexpr int HQ = SPLIT ? 4 : 2;
+    // t + WG/2).
+    static constexpr int HQ = 2;
     static constexpr int HROW = WG / HQ;  // counters per window row
     static constexpr int HIST_BYTES = W * HROW * 4;
     // Layout.  Default: [window rows | out-of-window bins (OUTL) | tables].
     // The digit-pair table needs at least EBT below it: S limbs are stored
     // biased by EBT and looked up at (TB - EBT) + S, an unsigned immediate
     // offset (b65-68: EBT exceeds the histogram region, so the table starts
-    // later).  SPLIT: [OUTL | pad | X1 at TB = EBT | X2 at TH | window rows]:
-    // the C limbs (unbiased) reach X2 at TH + C, so TH < 65536; X2 starts one
-    // entry before X1 ends (TB + 8B = 8 * 2^T = 65536), where both tables hold
-    // zeros (X1's last entry marks only digits >= 64, X2's first none).
-    static constexpr int TB0 = SPLIT ? 0 : (HIST_BYTES + 4 * NBINS + 15) / 16 * 16;
-    static constexpr int TB = SPLIT ? (int)EBT : (TB0 >= (int)EBT ? TB0 : ((int)EBT + 15) / 16 * 16);
-    static constexpr int TH = TB + (int)(B * ES) - ES;  // SPLIT: X2, the u16 high words
+    // later).  SPLIT: [OUTL | pad | X2 at T2 | X1 at TB | window rows]: S
+    // limbs (biased by EBT) are looked up at (TB - EBT) + S in X1 and at
+    // (T2 - EBT / 2) + S / 2 in X2, C limbs at TB + C and T2 + C / 2, all
+    // unsigned 16-bit immediate offsets.
+    static constexpr int T2 = SPLIT ? std::max((4 * NBINS + 15) / 16 * 16, ((int)EBT / 2 + 15) / 16 * 16) : 0;
+    static constexpr int TB0 = SPLIT ? (T2 + 4 * (int)B + 15) / 16 * 16 : (HIST_BYTES + 4 * NBINS + 15) / 16 * 16;
+    static constexpr int TB = TB0 >= (int)EBT ? TB0 : ((int)EBT + 15) / 16 * 16;
     static constexpr int OUTL = SPLIT ? 0 : HIST_BYTES;  // per-workgroup histogram of out-of-window counts
-    static constexpr int TC0 = TB / 16 * 16;  // the table image starts here (16-byte copy)
+    static constexpr int TC0 = (SPLIT ? T2 : TB) / 16 * 16;  // the table image starts here (16-byte copy)
     // Low-digit entry, word 1: digit bits [0, DB), then the carries and flags
     // of the step n -> n+1, all functions of n mod B (limb 0 of S, C, D1, N3
     // is never stored): the carry out of S limb 0 of S += D1 and the carry
@@ -298,7 +308,7 @@ struct Cfg {
     // (regions padded to 16 bytes: the image is copied in with 16-byte accesses)
     static constexpr int TL = TB + ((int)(B * ES) + 15) / 16 * 16;  // low-digit table (2B entries)
     static constexpr int TK = TL + (LSD ? ((int)(2 * B * ES) + 15) / 16 * 16 : 0);  // LSDX: carry bytes
-    static constexpr int TEND = SPLIT ? (TH + (int)(B * ES) + 15) / 16 * 16
+    static constexpr int TEND = SPLIT ? (TB + (int)(B * ES) + 15) / 16 * 16
                                       : TK + (LSDX ? ((int)(2 * B) + 15) / 16 * 16 : 0);
     static constexpr int HB = SPLIT ? TEND : 0;  // window rows
     static constexpr int LDS_BYTES = SPLIT ? HB + HIST_BYTES : TEND;
@@ -343,12 +353,11 @@ struct Cfg {
     // wave finishes: b54 1e9, one 1024-thread workgroup per CU, waited 61 us
     // of a 134 us workgroup life for it, profiles/r03/fd2_stamps_b54.log).
     // -1: the per-base default.
-    static constexpr bool PERS = PERS_ >= 0 ? PERS_ != 0 : (WG >= 1024 && !SPLIT && one_wg_per_cu(BASE, WG));
+    static constexpr bool PERS = PERS_ >= 0 ? PERS_ != 0 : (WG >= 1024 && one_wg_per_cu(BASE, WG));
     // the same kernel with rounds of workgroups (launch_cfg falls back to it
     // when the runtime occupancy or the field size does not suit PERS), at
     // the workgroup size rounds prefer
     using NoPers = Cfg<BASE_, ND_, NE_, NE2_, PROBE_, (PERS_ < 0 ? rounds_wg(BASE_) : WG_), VD_, LG_, 0>;
-    static_assert(!(PERS && SPLIT), "persistent lanes count more than a u8 counter holds");
     // VD & 256 (no low-digit table only): limb 0 of S and of C by VALU too --
     // n^2 mod B and n^3 mod B of a wave's lanes keep few residues mod 16, so
     // their lookups pile onto few bank quads
@@ -369,10 +378,11 @@ struct Cfg {
     static_assert(ND <= NX + 1 && NE2 <= NX + 1 && NE <= NS + 1, "difference limb counts");
     static_assert(S_TOPD >= 1 && C_TOPD >= 1, "top limb");
     static_assert(TB >= (int)EBT && TB - (int)EBT < 65536 && (!LSD || LSDX || TL < 65536), "LDS offsets");
-    static_assert(!SPLIT || (TH < 65536 && TB + (int)(B * ES) == ES << T && 4 * NBINS <= TC0 && TCHUNK <= 255),
+    static_assert(!SPLIT || (T2 >= (int)EBT / 2 && T2 < 65536 && T2 + 4 * (int)B <= TB && 4 * NBINS <= TC0 &&
+                             ES == 8 && TB < 65536),
                   "split layout");
     static_assert(LDS_BYTES <= 163840, "LDS");
-    static_assert((SPLIT || TB % 16 == 0) && TAB_BYTES % 16 == 0 && HB % 16 == 0, "16-byte table copy");
+    static_assert(TB % 16 == 0 && TAB_BYTES % 16 == 0 && HB % 16 == 0, "16-byte table copy");
     static_assert(W0 >= 0 && W0 + W <= NBINS, "window");
     static_assert(!LSD || (ES == 8 && (LSDX ? TIGHT && FC + FCW <= 6 : FC + FCW <= 30)), "low-digit entry layout");
     static_assert(C1 || ((unsigned long long)MAGICB * B - (1ull << 32)) * (TMAX / ES) < (1ull << 32),
@@ -414,16 +424,10 @@ template <class P>
 __device__ __forceinline__ void or_entry(const unsigned char *p, u32 (&m)[P::MW]) {
     if constexpr (P::MW == 1) {
         m[0] |= *(const u32 *)p;
-    } else if constexpr (P::MW == 2) {
+    } else if constexpr (P::MW == 2 || P::SPLIT) {
         uint2 v = *(const uint2 *)p;
         m[0] |= v.x;
         m[1] |= v.y;
-    } else if constexpr (P::SPLIT) {
-        // the same stored limb addresses both tables (two immediate offsets)
-        uint2 v = *(const uint2 *)p;
-        m[0] |= v.x;
-        m[1] |= v.y;
-        m[2] |= *(const unsigned short *)(p + (P::TH - P::TB));
     } else {
         uint4 v = *(const uint4 *)p;
         m[0] |= v.x;
@@ -434,6 +438,14 @@ __device__ __forceinline__ void or_entry(const unsigned char *p, u32 (&m)[P::MW]
         // over 32 banks (8 cycles per wave) instead of 4 groups over 64 (4).
         asm volatile("" ::"v"(v.w));
     }
+}
+
+// OR the digit-pair mask of a stored limb into m: X1 (or the one table) at
+// smem + OFF1 + stored; SPLIT also X2 at smem + OFF2 + stored / 2.
+template <class P, int OFF1, int OFF2>
+__device__ __forceinline__ void or_lookup(const unsigned char *smem, u32 stored, u32 (&m)[P::MW]) {
+    or_entry<P>(smem + OFF1 + stored, m);
+    if constexpr (P::SPLIT) m[2] |= *(const u32 *)(smem + OFF2 + (stored >> 1));
 }
 
 // End of a lookup group (Cfg::LG): the group's ORs are pinned here (the mask
@@ -470,7 +482,7 @@ __device__ __forceinline__ void or_valu(u32 vs, u32 (&m)[P::MW]) {
 template <class P>
 __device__ __forceinline__ void or_plain(const unsigned char *smem, u32 v, int digits, u32 (&m)[P::MW]) {
     if (digits == 2) {
-        or_entry<P>(smem + P::TB + v * P::ES, m);
+        or_lookup<P, P::TB, P::T2>(smem, v * P::ES, m);
     } else {
 #pragma unroll
         for (int w = 0; w < P::MW; w++) m[w] |= (v >> 5) == (u32)w ? 1u << (v & 31) : 0u;
@@ -779,12 +791,7 @@ __global__ void fd2_tables_kernel(unsigned char *tb) {
     };
     mark(e);
     put(tb + (P::TB - P::TC0) + e * P::ES);
-    if constexpr (P::SPLIT) {
-        // X2: the u16 high word (digits 64..) at the same stride; its entry 0
-        // shares its bytes with X1's last entry, zero in both (static_assert)
-        static_assert(P::BASE <= 80, "X2 holds the digits 64..79");
-        if (v[2]) *(unsigned short *)(tb + (P::TH - P::TC0) + e * P::ES) = (unsigned short)v[2];
-    }
+    if constexpr (P::SPLIT) *(u32 *)(tb + (P::T2 - P::TC0) + 4 * e) = v[2];  // X2: digits 64..
     if constexpr (P::LSD) {
         v[0] = v[1] = v[2] = v[3] = 0;
         const u32 B = P::B;
@@ -982,14 +989,14 @@ __device__ __forceinline__ void walk_chunk(State<P> &st, const unsigned char *sm
             for (int q = P::LO; q < P::SL; q++) {
                 if ((P::PROBE & 4) && q == 1) { m[0] |= st.S[q] & 0xffu; continue; }  // probe: no limb-1 lookups
                 if (q >= P::SL - P::VDS || (P::VDL && q == 0)) or_valu<P>(st.S[q] - P::EBT, m);
-                else or_entry<P>(smem + (P::TB - P::EBT) + st.S[q], m);
+                else or_lookup<P, P::TB - (int)P::EBT, P::T2 - (int)P::EBT / 2>(smem, st.S[q], m);
                 if (P::LG && (q - P::LO + 1) % P::LG == 0) lookup_group_end<P>(m);
             }
 #pragma unroll
             for (int q = P::LO; q < P::CL; q++) {
                 if ((P::PROBE & 4) && q == 1) { m[1] |= st.C[q] & 0xffu; continue; }
                 if (q >= P::CL - P::VDC || (P::VDL && q == 0)) or_valu<P>(st.C[q], m);
-                else or_entry<P>(smem + P::TB + st.C[q], m);
+                else or_lookup<P, P::TB, P::T2>(smem, st.C[q], m);
                 if (P::LG && (P::SL + q - 2 * P::LO + 1) % P::LG == 0) lookup_group_end<P>(m);
             }
         }

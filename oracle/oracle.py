@@ -13,7 +13,8 @@ import subprocess
 from dataclasses import dataclass
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+# NICE_ORACLE_LIB_PATH: a sanitizer build of the same source (scripts/sanitize.sh)
+_LIB_PATH = os.environ.get("NICE_ORACLE_LIB_PATH") or os.path.join(_HERE, "liboracle.so")
 _lib = None
 
 MASK64 = (1 << 64) - 1
@@ -28,9 +29,9 @@ def build() -> str:
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(
-            os.path.join(_HERE, "oracle.c")
-        ):
+        if not os.environ.get("NICE_ORACLE_LIB_PATH") and (
+                not os.path.exists(_LIB_PATH) or
+                os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "oracle.c"))):
             build()
         L = ctypes.CDLL(_LIB_PATH)
         u64, u32, i32, sz = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_size_t
