@@ -6,8 +6,8 @@
  * niceonly, on the GPU with --gpu or on the CPU path without it) reduced to
  * one call per mode, and what a cgo / Rust FFI binding would do first.
  *
- *   nice_field [--gpu] [--device D] detailed|niceonly BASE START END
- *   nice_field [--gpu] [--device D] detailed|niceonly BASE range [SIZE]
+ *   nice_field [--gpu] [--device D] [--repeat R] detailed|niceonly BASE START END
+ *   nice_field [--gpu] [--device D] [--repeat R] detailed|niceonly BASE range [SIZE]
  *
  * START / END are decimal u128; "range" takes the base's valid range
  * (get_base_range_u128, base_range.rs:14-54), truncated to SIZE numbers.
@@ -15,8 +15,12 @@
  * FieldResults.distribution), "nice N U" lines (ascending) and a "numbers
  * checked/sec" line (client/src/main.rs:363-370).  Without --gpu the
  * reference's CPU API is used (nice_cpu_process_range_*); with --gpu a
- * missing device is an error, never a silent CPU run.  Exit code: 0, or the
- * library's error code with nice_last_error() on stderr.
+ * missing device is an error, never a silent CPU run.  --repeat R then calls
+ * the same field R more times and prints the wall time per call (median and
+ * minimum over the R calls, clock_gettime around the library call: what a
+ * native caller waits) and, with --gpu detailed, the kernel time of each
+ * (nice_last_kernel_stats, HIP events).  Exit code: 0, or the library's error
+ * code with nice_last_error() on stderr.
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -64,16 +68,22 @@ static int fail(int rc, const char *what) {
 }
 
 static int usage(void) {
-    fprintf(stderr, "usage: nice_field [--gpu] [--device D] detailed|niceonly BASE START END\n"
-                    "       nice_field [--gpu] [--device D] detailed|niceonly BASE range [SIZE]\n");
+    fprintf(stderr, "usage: nice_field [--gpu] [--device D] [--repeat R] detailed|niceonly BASE START END\n"
+                    "       nice_field [--gpu] [--device D] [--repeat R] detailed|niceonly BASE range [SIZE]\n");
     return NICE_ERR_INVALID;
 }
 
+static int cmp_double(const void *a, const void *b) {
+    const double x = *(const double *)a, y = *(const double *)b;
+    return x < y ? -1 : x > y;
+}
+
 int main(int argc, char **argv) {
-    int gpu = 0, device = 0, a = 1;
+    int gpu = 0, device = 0, a = 1, repeat = 0;
     for (; a < argc && strncmp(argv[a], "--", 2) == 0; a++) {
         if (strcmp(argv[a], "--gpu") == 0) gpu = 1;
         else if (strcmp(argv[a], "--device") == 0 && a + 1 < argc) device = atoi(argv[++a]);
+        else if (strcmp(argv[a], "--repeat") == 0 && a + 1 < argc) repeat = atoi(argv[++a]);
         else return usage();
     }
     if (argc - a < 3) return usage();
@@ -154,6 +164,45 @@ int main(int argc, char **argv) {
     }
     const double secs = t1 - t0;
     printf("numbers checked/sec %.6g (%.6f s)\n", secs > 0 ? (double)(end - start) / secs : 0.0, secs);
+    if (repeat > 0) {
+        double *wall = (double *)malloc((size_t)repeat * sizeof *wall);
+        double *kern = (double *)malloc((size_t)repeat * sizeof *kern);
+        int nk = 0;
+        for (int r = 0; r < repeat && rc == NICE_OK; r++) {
+            size_t m = 0;
+            t0 = now_s();
+            if (detailed && gpu)
+                rc = nice_process_range_detailed(ctx, s_lo, s_hi, e_lo, e_hi, base, hist, list, cap, &m);
+            else if (detailed)
+                rc = nice_cpu_process_range_detailed(s_lo, s_hi, e_lo, e_hi, base, 0, hist, list, cap, &m);
+            else if (gpu)
+                rc = nice_process_range_niceonly(ctx, s_lo, s_hi, e_lo, e_hi, base, list, cap, &m);
+            else
+                rc = nice_cpu_process_range_niceonly(s_lo, s_hi, e_lo, e_hi, base, 0, 0, list, cap, &m);
+            wall[r] = now_s() - t0;
+            if (rc == NICE_OK && m != n) rc = NICE_ERR_INVALID;  /* the same field, the same list */
+            nice_kernel_stats ks;
+            if (rc == NICE_OK && detailed && gpu && nice_last_kernel_stats(ctx, 0, &ks) == NICE_OK)
+                kern[nk++] = ks.kernel_ms * 1e-3;
+        }
+        if (rc != NICE_OK) {
+            free(wall);
+            free(kern);
+            free(list);
+            if (ctx) nice_ctx_destroy(ctx);
+            return fail(rc, "repeat");
+        }
+        qsort(wall, (size_t)repeat, sizeof *wall, cmp_double);
+        printf("repeat %d: wall per call median %.2f us, min %.2f us", repeat, wall[repeat / 2] * 1e6,
+               wall[0] * 1e6);
+        if (nk) {
+            qsort(kern, (size_t)nk, sizeof *kern, cmp_double);
+            printf("; kernel median %.2f us", kern[nk / 2] * 1e6);
+        }
+        printf("\n");
+        free(wall);
+        free(kern);
+    }
     free(list);
     if (ctx) nice_ctx_destroy(ctx);
     return 0;

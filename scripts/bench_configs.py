@@ -3,11 +3,14 @@ headline extra-large config; these are the others).  One JSON line per config:
 numbers/s = field size / median wall seconds of the library call (same
 definition as the reference's log line, client/src/main.rs:363-370).
 
-  python scripts/bench_configs.py [--massive-sample 1e11] [--reps 5]
+  python scripts/bench_configs.py [--reps 5] [--massive-world 8]
 
-massive (b50, 1e13, niceonly) runs on a bounded prefix of the field with the
-full field's client chunk (1e8, client/src/main.rs:159-168), so MSD leaves
-and candidates are the ones the whole field would produce there."""
+massive (b50, 1e13, niceonly) runs the WHOLE field with its client chunk
+(1e8, client/src/main.rs:159-168) on one GPU, its candidate and range totals
+asserted against tests/golden/massive_b50.json (the oracle's fixture), then
+each of the --massive-world ranks' dealt shares (chunks c = r mod N, what
+rank r of an N-GPU job processes, nice_amd/dist.py) timed alone: the
+N-GPU time of the field is the slowest share, not an extrapolation."""
 import argparse
 import json
 import os
@@ -34,7 +37,7 @@ def timed(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--massive-sample", type=float, default=1e11)
+    ap.add_argument("--massive-world", type=int, default=8)
     ap.add_argument("--bases", default="", help="also: detailed 1e9 at the range start of these "
                     "bases ('all' = every FD base), with the W_alg roofline fraction")
     ap.add_argument("--nice-bases", default="", help="also: niceonly 1e10 at 1/3 of the range "
@@ -94,12 +97,28 @@ def main():
     det("hi-base-1e6", get_benchmark_field(BM.HI_BASE, hi_base_size=10 ** 6), "BASELINE size")
     det("hi-base-1e9", get_benchmark_field(BM.HI_BASE), "benchmark.rs:63 size")
     m = get_benchmark_field(BM.MASSIVE)
-    size = int(a.massive_sample)
-    sample = type(m)(claim_id=0, base=50, range_start=m.range_start,
-                     range_end=m.range_start + size, range_size=size)
-    nice("massive-sample", sample, chunk=10 ** 8, reps=3,
-         note=f"first {size:.0e} n of the 1e13 b50 field, client chunk 1e8; "
-              f"full field on 8 GPUs ~ 1e13 / (8 x numbers_per_sec)")
+    with open(os.path.join(ROOT, "tests", "golden", "massive_b50.json")) as fh:
+        fx = json.load(fh)
+    want = (sum(w["candidates"] for w in fx["windows"]), sum(w["ranges"] for w in fx["windows"]))
+    nice("massive", m, chunk=10 ** 8, reps=3, note="whole 1e13 b50 field on one GPU, client chunk 1e8")
+    assert (out[-1]["candidates"], out[-1]["msd_ranges"]) == want, (out[-1], want)
+    t1 = out[-1]["wall_ms"]
+    W = a.massive_world
+    shares = []
+    for r in range(W):
+        sec, (lst, st) = timed(lambda: ctx.niceonly_raw(m.range_start, m.range_end, 50, chunk_size=10 ** 8,
+                                                         deal_stride=W, deal_offset=r), 3)
+        shares.append({"rank": r, "wall_ms": sec * 1e3, "candidates": st.candidates, "msd_ranges": st.ranges,
+                       "nice": len(lst)})
+    assert (sum(x["candidates"] for x in shares), sum(x["msd_ranges"] for x in shares)) == want
+    tmax = max(x["wall_ms"] for x in shares)
+    out.append({"config": f"massive-dealt-{W}", "mode": "niceonly", "base": 50, "size": m.range_size,
+                "world": W, "max_share_wall_ms": tmax, "t1_wall_ms": t1,
+                "numbers_per_sec": m.range_size / (tmax / 1e3),
+                "projected_efficiency": t1 / (W * tmax), "shares": shares,
+                "note": f"each of {W} ranks' dealt share of the whole field timed alone on one GPU; "
+                        f"numbers_per_sec = field / slowest share (the {W}-GPU field time without "
+                        f"the exchange)"})
     nice("msd-effective", get_benchmark_field(BM.MSD_EFFECTIVE), reps=3)
     nice("msd-ineffective", get_benchmark_field(BM.MSD_INEFFECTIVE))
     for r in out:
