@@ -6,8 +6,8 @@
  * niceonly, on the GPU with --gpu or on the CPU path without it) reduced to
  * one call per mode, and what a cgo / Rust FFI binding would do first.
  *
- *   nice_field [--gpu] [--device D] [--repeat R] detailed|niceonly BASE START END
- *   nice_field [--gpu] [--device D] [--repeat R] detailed|niceonly BASE range [SIZE]
+ *   nice_field [--gpu] [--device D] [--repeat R] [--no-timing] detailed|niceonly BASE START END
+ *   nice_field [--gpu] [--device D] [--repeat R] [--no-timing] detailed|niceonly BASE range [SIZE]
  *
  * START / END are decimal u128; "range" takes the base's valid range
  * (get_base_range_u128, base_range.rs:14-54), truncated to SIZE numbers.
@@ -19,8 +19,9 @@
  * the same field R more times and prints the wall time per call (median and
  * minimum over the R calls, clock_gettime around the library call: what a
  * native caller waits) and, with --gpu detailed, the kernel time of each
- * (nice_last_kernel_stats, HIP events).  Exit code: 0, or the library's error
- * code with nice_last_error() on stderr.
+ * (nice_last_kernel_stats, HIP events); --no-timing turns the context's kernel
+ * timing off (nice_ctx_set_kernel_timing: no events per field).  Exit code: 0,
+ * or the library's error code with nice_last_error() on stderr.
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -68,8 +69,10 @@ static int fail(int rc, const char *what) {
 }
 
 static int usage(void) {
-    fprintf(stderr, "usage: nice_field [--gpu] [--device D] [--repeat R] detailed|niceonly BASE START END\n"
-                    "       nice_field [--gpu] [--device D] [--repeat R] detailed|niceonly BASE range [SIZE]\n");
+    fprintf(stderr, "usage: nice_field [--gpu] [--device D] [--repeat R] [--no-timing] detailed|niceonly BASE "
+                    "START END\n"
+                    "       nice_field [--gpu] [--device D] [--repeat R] [--no-timing] detailed|niceonly BASE "
+                    "range [SIZE]\n");
     return NICE_ERR_INVALID;
 }
 
@@ -79,11 +82,12 @@ static int cmp_double(const void *a, const void *b) {
 }
 
 int main(int argc, char **argv) {
-    int gpu = 0, device = 0, a = 1, repeat = 0;
+    int gpu = 0, device = 0, a = 1, repeat = 0, timing = 1;
     for (; a < argc && strncmp(argv[a], "--", 2) == 0; a++) {
         if (strcmp(argv[a], "--gpu") == 0) gpu = 1;
         else if (strcmp(argv[a], "--device") == 0 && a + 1 < argc) device = atoi(argv[++a]);
         else if (strcmp(argv[a], "--repeat") == 0 && a + 1 < argc) repeat = atoi(argv[++a]);
+        else if (strcmp(argv[a], "--no-timing") == 0) timing = 0;
         else return usage();
     }
     if (argc - a < 3) return usage();
@@ -116,6 +120,11 @@ int main(int argc, char **argv) {
     if (gpu) {
         const int rc = nice_ctx_create(&device, 1, &ctx);
         if (rc != NICE_OK) return fail(rc, "nice_ctx_create");
+        const int rt = timing ? NICE_OK : nice_ctx_set_kernel_timing(ctx, 0);
+        if (rt != NICE_OK) {
+            nice_ctx_destroy(ctx);
+            return fail(rt, "nice_ctx_set_kernel_timing");
+        }
     }
     uint64_t hist[129];
     memset(hist, 0, sizeof hist);
@@ -182,7 +191,7 @@ int main(int argc, char **argv) {
             wall[r] = now_s() - t0;
             if (rc == NICE_OK && m != n) rc = NICE_ERR_INVALID;  /* the same field, the same list */
             nice_kernel_stats ks;
-            if (rc == NICE_OK && detailed && gpu && nice_last_kernel_stats(ctx, 0, &ks) == NICE_OK)
+            if (rc == NICE_OK && detailed && gpu && timing && nice_last_kernel_stats(ctx, 0, &ks) == NICE_OK)
                 kern[nk++] = ks.kernel_ms * 1e-3;
         }
         if (rc != NICE_OK) {

@@ -205,14 +205,21 @@ int nice_niceonly_collect(nice_ctx *ctx, int ticket, nice_number *out, size_t ca
                           nice_niceonly_stats *stats);
 
 /* Device time of the hot kernel(s) of the last collected detailed field on a
- * device, measured with HIP events on the launch stream. */
+ * device, measured with HIP events on the launch stream (kernel_ms 0 when the
+ * field ran with kernel timing off). */
 typedef struct {
-    double kernel_ms;    /* summed over launches */
+    double kernel_ms;    /* summed over launches; 0 when the field was not timed */
     uint32_t launches;
     uint32_t fd_kernel;  /* 1 if the finite-difference kernel ran */
     uint64_t numbers;    /* numbers processed by those launches */
 } nice_kernel_stats;
 int nice_last_kernel_stats(nice_ctx *ctx, int device_index, nice_kernel_stats *out);
+/* Kernel timing of later detailed fields on this context (default on): with
+ * it off a field records no HIP events -- two fewer runtime calls on the
+ * submit path of every field, which is what a latency-bound caller of small
+ * fields pays for (the reference client never reads kernel times) -- and
+ * nice_last_kernel_stats reports kernel_ms 0. */
+int nice_ctx_set_kernel_timing(nice_ctx *ctx, int enable);
 
 /* Host helpers mirroring the reference functions the client calls. */
 /* get_base_range_u128 (base_range.rs:43-54): 1 range, 0 none, -1 exceeds u128. */

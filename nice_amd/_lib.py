@@ -35,7 +35,7 @@ EXPORTS = (
     "nice_fd_segment_cuts", "nice_validate_detailed", "nice_detailed_submit",
     "nice_detailed_collect", "nice_niceonly_submit", "nice_niceonly_collect",
     "nice_cpu_process_range_detailed", "nice_cpu_process_range_niceonly",
-    "nice_adaptive_floor_step", "nice_adaptive_floor",
+    "nice_adaptive_floor_step", "nice_adaptive_floor", "nice_ctx_set_kernel_timing",
 )
 
 
@@ -111,6 +111,7 @@ def lib():
                                             ctypes.POINTER(nice_niceonly_opts), PN, sz, PSZ,
                                             ctypes.POINTER(nice_niceonly_stats)], i32),
         "nice_last_kernel_stats": ([vp, i32, ctypes.POINTER(nice_kernel_stats)], i32),
+        "nice_ctx_set_kernel_timing": ([vp, i32], i32),
         "nice_base_range": ([u32, P64, P64, P64, P64], i32),
         "nice_near_miss_cutoff": ([u32], u32),
         "nice_gpu_batch_size": ([], u64),

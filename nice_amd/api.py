@@ -185,6 +185,11 @@ class GpuContext:
             self._out_cap = cap
         return self._out
 
+    def set_kernel_timing(self, enable: bool):
+        """HIP-event timing of later detailed fields (default on; off saves two
+        runtime calls per field, and kernel_stats().kernel_ms reads 0)."""
+        check(lib().nice_ctx_set_kernel_timing(self._h, 1 if enable else 0))
+
     def kernel_stats(self, device_index: int = 0) -> KernelStats:
         s = _lib.nice_kernel_stats()
         check(lib().nice_last_kernel_stats(self._h, device_index, s))

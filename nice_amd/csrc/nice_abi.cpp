@@ -64,17 +64,6 @@ inline bool spin_wait() {
 #endif
 }
 
-// Probe build: NICE_NOTIME=1 skips the start event of a detailed field,
-// 2 also records its end on a non-timing event (kernel_ms reads 0).
-inline int no_time() {
-#ifdef NICE_PROBES
-    static const int v = getenv("NICE_NOTIME") ? atoi(getenv("NICE_NOTIME")) : 0;
-    return v;
-#else
-    return 0;
-#endif
-}
-
 // Streams of a device's slots: bit 0 = the slots share ONE detailed stream
 // (consecutive detailed fields run back to back instead of overlapping at
 // their edges), bit 1 = they share one niceonly stream.
@@ -170,6 +159,8 @@ struct Slot {
     uint32_t *d_msd_mapped = nullptr, *d_nice_mapped = nullptr;  // device views
     uint32_t *d_nice_done = nullptr;  // workgroups retired (niceonly in-kernel finish)
     bool dirty = true;            // state block not known to be zero
+    bool timed = false;           // the detailed field records ev0 / ev1 (kernel timing)
+    bool marked = false;          // ... or an untimed end marker (ev_done) on a shared stream
     uint64_t seq = 0;             // last detailed field's sequence number
     uint32_t launches = 0;        // ... and its kernel launches (the finish kernel not counted)
     bool fin_seq = false;         // ... and whether its fd2 finish publishes it
@@ -245,6 +236,7 @@ struct NiceJob {
 struct nice_ctx {
     std::vector<Device> devs;
     std::mutex mu;  // serialises calls on one context (client_process_gpu.rs:196-201)
+    bool timing = true;  // record HIP events around each detailed field (nice_ctx_set_kernel_timing)
     DetJob det[kSlots];
     NiceJob nice[kSlots];
     int det_next = 0, nice_next = 0;
@@ -531,31 +523,17 @@ int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *f
     return launch(std::max(s, re), e, false);
 }
 
-// The event after a detailed field's last launch: the kernel end (ev1) when
-// fd2 finished the field in-kernel, else the finish kernel's (ev_done).
-inline hipEvent_t done_event(const Slot &sl) { return sl.fin_seq && no_time() != 2 ? sl.ev1 : sl.ev_done; }
-
-// The kernel time of the device's last collected field, read from its slot's
-// events on demand (collect returns as soon as the results are published,
-// possibly before the end-of-kernel event has completed).
-int resolve_stats(Device &d) {
-    if (d.stats_slot < 0) return NICE_OK;
-    Slot &sl = d.slot[d.stats_slot];
-    d.stats_slot = -1;
-    HIPCHK(hipSetDevice(d.id));
-    HIPCHK(hipEventSynchronize(done_event(sl)));
-    float ms = 0;
-    if (!no_time()) HIPCHK(hipEventElapsedTime(&ms, sl.ev0, sl.ev1));
-    d.last.kernel_ms = ms;
-    return NICE_OK;
+// The event after a detailed field's last launch: the finish kernel's
+// (ev_done) when the field needed one; else the kernel end (ev1) of a timed
+// field, the end marker (ev_done) of an untimed one on a shared stream, or
+// none: an untimed field that fd2 finishes in-kernel on its slot's own stream
+// records no event at all (two fewer runtime calls per field), and the stream
+// itself reports its completion.
+inline hipEvent_t done_event(const Slot &sl) {
+    if (!sl.fin_seq) return sl.ev_done;
+    return sl.timed ? sl.ev1 : (sl.marked ? sl.ev_done : nullptr);
 }
 
-// Wait until the detailed field in slot `sl` is finished.  A field ending in
-// fd2's in-kernel finish is waited for by polling the sequence word that
-// finish publishes in mapped memory -- microseconds sooner than the kernel's
-// completion signal (which still follows: the last workgroup retires after
-// publishing).  The completion event is queried every 4096 polls, so a failed
-// launch or a finish that never publishes is reported, not spun on.
 // Polls spin for the first kSpinPolls (a small field ends within tens of
 // microseconds, and a sleeping waiter would add its wake-up latency), then
 // yield the core between polls.
@@ -575,16 +553,52 @@ hipError_t sync_event(hipEvent_t ev) {
     }
 }
 
+// A detailed field's completion: its end event, or its slot's own stream
+// when it recorded none (done_event).
+hipError_t field_query(const Slot &sl) {
+    const hipEvent_t ev = done_event(sl);
+    return ev ? hipEventQuery(ev) : hipStreamQuery(sl.stream);
+}
+
+hipError_t field_sync(const Slot &sl) {
+    for (uint32_t i = 0;; i++) {
+        const hipError_t q = field_query(sl);
+        if (q != hipErrorNotReady) return q;
+        backoff(i);
+    }
+}
+
+// The kernel time of the device's last collected field, read from its slot's
+// events on demand (collect returns as soon as the results are published,
+// possibly before the end-of-kernel event has completed).
+int resolve_stats(Device &d) {
+    if (d.stats_slot < 0) return NICE_OK;
+    Slot &sl = d.slot[d.stats_slot];
+    d.stats_slot = -1;
+    HIPCHK(hipSetDevice(d.id));
+    HIPCHK(field_sync(sl));
+    float ms = 0;
+    if (sl.timed) HIPCHK(hipEventElapsedTime(&ms, sl.ev0, sl.ev1));
+    d.last.kernel_ms = ms;
+    return NICE_OK;
+}
+
+// Wait until the detailed field in slot `sl` is finished.  A field ending in
+// fd2's in-kernel finish is waited for by polling the sequence word that
+// finish publishes in mapped memory -- microseconds sooner than the kernel's
+// completion signal (which still follows: the last workgroup retires after
+// publishing).  The completion event is queried every 4096 polls, so a failed
+// launch or a finish that never publishes is reported, not spun on.
 int wait_field(Slot &sl) {
     if (!sl.fin_seq || !spin_wait()) {
-        const hipError_t q = sync_event(done_event(sl));
+        const hipError_t q = field_sync(sl);
         if (q != hipSuccess) return fail(NICE_ERR_HIP, std::string("detailed field: ") + hipGetErrorString(q));
         return NICE_OK;
     }
     for (uint32_t i = 1;; i++) {
         if (__atomic_load_n(&sl.h_fin[130], __ATOMIC_ACQUIRE) == sl.seq) return NICE_OK;
         if ((i & 4095) == 0 || i > kSpinPolls) {
-            const hipError_t q = hipEventQuery(done_event(sl));
+            const hipError_t q = field_query(sl);
             if (q == hipSuccess) {
                 if (__atomic_load_n(&sl.h_fin[130], __ATOMIC_ACQUIRE) == sl.seq) return NICE_OK;
                 return fail(NICE_ERR_HIP, "detailed field completed without publishing its results");
@@ -596,7 +610,7 @@ int wait_field(Slot &sl) {
 }
 
 // Enqueue one device's shard of a detailed field into slot `sl` (async).
-int enqueue_detailed_shard(Device &d, Slot &sl, u128 s, u128 e, uint32_t base) {
+int enqueue_detailed_shard(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool timing) {
     HIPCHK(hipSetDevice(d.id));
     // this slot's events are about to be re-recorded
     if (d.stats_slot == (int)(&sl - d.slot)) {
@@ -609,15 +623,22 @@ int enqueue_detailed_shard(Device &d, Slot &sl, u128 s, u128 e, uint32_t base) {
     // only after an interrupted field (or the first one).
     if (sl.dirty) HIPCHK(hipMemsetAsync(sl.d_state, 0, kStateBytes, sl.stream));
     sl.dirty = true;
-    if (!no_time()) HIPCHK(hipEventRecord(sl.ev0, sl.stream));
+    sl.timed = timing;
+    sl.marked = false;
+    if (timing) HIPCHK(hipEventRecord(sl.ev0, sl.stream));
     bool finished = false;
     int rc = enqueue_detailed(d, sl, s, e, base, &finished);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(no_time() == 2 ? sl.ev_done : sl.ev1, sl.stream));
+    if (timing) HIPCHK(hipEventRecord(sl.ev1, sl.stream));
     sl.fin_seq = finished;
     if (!finished) {
         HIPCHK(nice::launch_detailed_finish(sl.d_state, sl.d_count, sl.d_fin, sl.stream));
         HIPCHK(hipEventRecord(sl.ev_done, sl.stream));
+    } else if (!timing && !sl.own_stream) {
+        // a stream shared between slots (probe build) cannot tell this
+        // field's completion from a later one's: mark its end
+        HIPCHK(hipEventRecord(sl.ev_done, sl.stream));
+        sl.marked = true;
     }
     return NICE_OK;
 }
@@ -634,7 +655,8 @@ int detailed_submit(nice_ctx *ctx, u128 s, u128 e, uint32_t base, int *ticket) {
     for (size_t i = 0; i <= nd; i++) job.bounds[i] = s + size / nd * i + std::min<u128>(i, size % nd);
     for (size_t i = 0; i < nd; i++) {
         if (job.bounds[i] >= job.bounds[i + 1]) continue;
-        int rc = enqueue_detailed_shard(ctx->devs[i], ctx->devs[i].slot[t], job.bounds[i], job.bounds[i + 1], base);
+        int rc = enqueue_detailed_shard(ctx->devs[i], ctx->devs[i].slot[t], job.bounds[i], job.bounds[i + 1], base,
+                                        ctx->timing);
         if (rc) return rc;
     }
     job.active = true;
@@ -674,7 +696,7 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
             // grow to the exact count and redo this shard (behind any field
             // queued after it; only this slot's completion is awaited).
             rc = ensure_listbuf(d, sl.det, cnt, true);
-            if (!rc) rc = enqueue_detailed_shard(d, sl, job.bounds[i], job.bounds[i + 1], base);
+            if (!rc) rc = enqueue_detailed_shard(d, sl, job.bounds[i], job.bounds[i + 1], base, sl.timed);
             if (!rc) rc = wait_field(sl);
             if (rc) return rc;
             sl.dirty = false;
@@ -687,7 +709,7 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
         if (cnt) {
             // the list is read after the kernel has retired (its end-of-kernel
             // cache write-back), not merely published its count
-            HIPCHK(hipEventSynchronize(done_event(sl)));
+            HIPCHK(field_sync(sl));
             std::vector<uint64_t> nbuf((size_t)cnt * 2);
             std::vector<uint32_t> ubuf(cnt);
             HIPCHK(hipMemcpy(nbuf.data(), sl.det.n, (size_t)cnt * 16, hipMemcpyDeviceToHost));
@@ -843,6 +865,13 @@ uint64_t nice_gpu_batch_size(void) { return 50000000ull; }
 uint64_t nice_processing_chunk_size(void) { return 1000000ull; }
 int nice_gpu_supports_base(uint32_t base) { return base >= 2 && base <= 128; }
 int nice_fd_kernel_base(uint32_t base) { return nice::fd2_supported(base) ? 1 : 0; }
+
+int nice_ctx_set_kernel_timing(nice_ctx *ctx, int enable) {
+    if (!ctx) return fail(NICE_ERR_INVALID, "null ctx");
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    ctx->timing = enable != 0;
+    return NICE_OK;
+}
 
 int nice_last_kernel_stats(nice_ctx *ctx, int i, nice_kernel_stats *out) {
     if (!ctx || i < 0 || i >= (int)ctx->devs.size() || !out) return fail(NICE_ERR_INVALID, "bad args");

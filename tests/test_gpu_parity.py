@@ -577,6 +577,43 @@ def test_collect_waits_without_holding_the_context(ctx):
     assert [out[i].number_lo | (out[i].number_hi << 64) for i in range(n.value)] == want_nice
 
 
+def test_untimed_fields_match_timed():
+    """With kernel timing off (nice_ctx_set_kernel_timing) a detailed field
+    records no HIP events; its completion comes from the published sequence
+    word and the slot's stream.  Results must equal the timed context's,
+    including fields with near-miss lists (read after the stream drains),
+    generic-kernel fields (finish kernel) and asynchronous tickets; kernel_ms
+    reads 0."""
+    c = N.GpuContext(0)
+    c.set_kernel_timing(False)
+    s40, s80 = O.base_range(40)[0], O.base_range(80)[0]
+    cases = [(s40, s40 + 10 ** 6, 40), (s80, s80 + 10 ** 6, 80), (10 ** 6, 10 ** 6 + 10 ** 4, 10),
+             (s40 - 5000, s40 + 5000, 40), (s40, s40 + 10 ** 9, 40)]
+    for a, b, base in cases:
+        want = O.process_range_detailed(a, b, base, cap=b - a) if b - a <= 10 ** 6 else None
+        got = c.detailed_raw(a, b, base)
+        if want is not None:
+            assert got == ([0] + [n for _, n in want.distribution], want.nice_numbers), (base, a, b)
+        else:
+            assert got == ctx_timed_detailed(a, b, base)
+        assert c.kernel_stats().kernel_ms == 0
+    t = [c.detailed_submit(a, b, base) for a, b, base in cases[:3]]
+    assert [c.detailed_collect(x, base) for x, (_, _, base) in zip(t, cases[:3])] == \
+        [c.detailed_raw(a, b, base) for a, b, base in cases[:3]]
+    c.set_kernel_timing(True)
+    c.detailed_raw(*cases[0])
+    assert c.kernel_stats().kernel_ms > 0
+    c.close()
+
+
+def ctx_timed_detailed(a, b, base):
+    c = N.GpuContext(0)
+    try:
+        return c.detailed_raw(a, b, base)
+    finally:
+        c.close()
+
+
 def test_multi_device_context_sharding():
     import torch
     n = torch.cuda.device_count()
