@@ -1,9 +1,11 @@
 """Small-field host latency (probe build): median wall of the synchronous
 detailed call and of its submit / collect halves, for b40 / b80 at 1e4..1e8,
 with collect waiting by polling the published sequence word (NICE_SPIN=1,
-default) or by the completion event (NICE_SPIN=0).  Also the cost of a
-ctypes no-op call (the Python binding's floor).  Usage:
-    NICE_SPIN=0|1 python scripts/latency_probe.py [--product]"""
+default) or by the completion event (NICE_SPIN=0), with the context's kernel
+timing on or off (--untimed: nice_ctx_set_kernel_timing(0), no HIP events per
+field).  Also the cost of a ctypes no-op call (the Python binding's floor).
+Usage:
+    NICE_SPIN=0|1 python scripts/latency_probe.py [--product] [--untimed]"""
 import os
 import statistics
 import sys
@@ -25,9 +27,11 @@ for _ in range(10000):
 noop_us = (time.perf_counter() - t) / 10000 * 1e6
 tag = "product" if "--product" in sys.argv else \
     f"spin={os.environ.get('NICE_SPIN', '1')} nofin={os.environ.get('NICE_FD2_NOFIN', '0')} "\
-    f"notime={os.environ.get('NICE_NOTIME', '0')}"
+    f"untimed={int('--untimed' in sys.argv)}"
 print(f"[{tag}] ctypes no-op call: {noop_us:.2f} us", flush=True)
 ctx = N.GpuContext(0)
+if "--untimed" in sys.argv:
+    ctx.set_kernel_timing(False)
 for base, size in ((40, 10 ** 4), (40, 10 ** 6), (80, 10 ** 6), (40, 10 ** 8)):
     s = N.get_base_range_u128(base).range_start
     ref = ctx.detailed_raw(s, s + size, base)
