@@ -821,6 +821,22 @@ def test_fd_bases_whole_fields_1e9(ctx):
         assert ctx.kernel_stats().fd_kernel == 1
 
 
+def test_fd_bases_more_whole_fields_1e9(ctx):
+    """One 1e9 field per FD kernel class the CLI fields do not cover (b42:
+    TCHUNK 80; b49: 160; b59: 240 with the side-table low-digit path; b65:
+    three mask words), one third into each range, all on the persistent grid:
+    distribution and near-miss list against the oracle fixture
+    (gen_fd_bases_fixtures.py --more)."""
+    p = os.path.join(ROOT, "tests", "golden", "fd_bases_more_1e9.json")
+    with open(p) as f:
+        fx = json.load(f)
+    for c in fx["detailed"]:
+        hist, lst = ctx.detailed_raw(int(c["start"]), int(c["end"]), c["base"])
+        assert _dist(hist) == [tuple(x) for x in c["distribution"]], c["name"]
+        assert lst == [(int(n), u) for n, u in c["near_misses"]], c["name"]
+        assert ctx.kernel_stats().fd_kernel == 1
+
+
 # --- massive config (benchmark.rs:62): b50 [start, +1e13), niceonly ----------
 def _massive():
     p = os.path.join(ROOT, "tests", "golden", "massive_b50.json")

@@ -235,3 +235,25 @@ def test_fd_bases_fixture_consistent():
     pre = O.process_range_detailed(s, s + 10 ** 5, 80)
     full = dict((u, n) for u, n in b80["distribution"])
     assert all(n <= full[u] for u, n in pre.distribution)
+
+
+def test_fd_bases_more_fixture_consistent():
+    """tests/golden/fd_bases_more_1e9.json (gen_fd_bases_fixtures.py --more):
+    1e9 fields one third into the ranges of b42 / b49 / b59 / b65, each
+    distribution summing to 1e9 with the near-miss list matching the bins above
+    the cutoff, and every near-miss recomputing by the oracle."""
+    import json
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fd_bases_more_1e9.json")
+    fx = json.load(open(p))
+    assert [c["base"] for c in fx["detailed"]] == [42, 49, 59, 65]
+    for c in fx["detailed"]:
+        b = c["base"]
+        r0, r1 = O.base_range(b)
+        s = int(c["start"])
+        assert s == r0 + (r1 - r0) // 3 and int(c["end"]) == s + 10 ** 9
+        assert [u for u, _ in c["distribution"]] == list(range(1, b + 1))
+        assert sum(n for _, n in c["distribution"]) == 10 ** 9
+        cut = O.near_miss_cutoff(b)
+        assert sum(n for u, n in c["distribution"] if u > cut) == len(c["near_misses"])
+        assert all(O.num_unique_digits(int(n), b) == u > cut for n, u in c["near_misses"])
