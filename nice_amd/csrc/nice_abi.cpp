@@ -875,6 +875,9 @@ int nice_ctx_set_kernel_timing(nice_ctx *ctx, int enable) {
 
 int nice_last_kernel_stats(nice_ctx *ctx, int i, nice_kernel_stats *out) {
     if (!ctx || i < 0 || i >= (int)ctx->devs.size() || !out) return fail(NICE_ERR_INVALID, "bad args");
+    // (under the context lock: a collect on another thread updates the
+    // device's last-field record)
+    std::lock_guard<std::mutex> lock(ctx->mu);
     int rc = resolve_stats(ctx->devs[i]);
     if (rc) return rc;
     *out = ctx->devs[i].last;
