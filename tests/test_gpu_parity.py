@@ -980,3 +980,99 @@ def test_fd_kernel_fuzz_windows(ctx):
         a = s + rng.randrange(e - s - size)
         want = O.process_field_detailed_mt(a, a + size, base, 8, cap=size)
         check_detailed(ctx, a, a + size, base, want=want)
+
+
+def test_niceonly_fuzz_every_base(ctx):
+    """Seeded niceonly fuzz over every base 3..97 with a valid range (and the
+    residue-empty ones, which must return nothing): per base a window at a
+    random offset of its range, size log-uniform over 1 .. 3e7, through both
+    MSD placements; nice list, stride candidates and MSD ranges against the
+    oracle on the same client chunk grid (client_process.rs:439-465 per chunk,
+    client/src/main.rs:158-168 chunking)."""
+    rng = random.Random(4_20261017)
+    checked = 0
+    for base in range(3, 98):
+        r = O.base_range(base)
+        if r is None:
+            continue
+        s, e = r
+        size = min(e - s, max(1, int(10 ** rng.uniform(0, 7.48))))
+        a = s + rng.randrange(e - s - size + 1)
+        res, cands, ranges, _ = O.process_field_niceonly_sq(a, a + size, base, 8, 0, 0, cap=1 << 20)
+        want = [n for n, _ in res.nice_numbers]
+        for where in MSD_WHERE:
+            lst, st = ctx.niceonly_raw(a, a + size, base, msd_where=where)
+            assert lst == want, (base, a, size, where)
+            if O.residue_filter(base):
+                assert (st.candidates, st.ranges) == (cands, ranges), (base, a, size, where)
+        checked += 1
+    assert checked > 60
+
+
+def test_threads_share_a_context():
+    """Four host threads drive ONE context at once, each submitting and
+    collecting its own detailed and niceonly fields (raw ABI calls, per-thread
+    buffers): with collects waiting outside the context lock the submits,
+    waits and gathers interleave freely, and every result must equal the
+    single-threaded one.  (The reference shares its GpuContext as an Arc
+    across the client's tasks, client/src/main.rs:622.)"""
+    import threading
+    import time
+    lib = N._lib.lib()
+    ct = N._lib.ctypes
+    c = N.GpuContext(0)
+    s40, s80 = O.base_range(40)[0], O.base_range(80)[0]
+    jobs = [(s40 + k * 3 * 10 ** 6, s40 + (k * 3 + 1) * 10 ** 6, 40) for k in range(6)] + \
+           [(s80 + k * 10 ** 6, s80 + k * 10 ** 6 + 5 * 10 ** 5, 80) for k in range(4)] + \
+           [(10 ** 6, 10 ** 6 + 10 ** 4, 10)]
+    want_det = [c.detailed_raw(a, b, base) for a, b, base in jobs]
+    want_nice = [c.niceonly_raw(a, b, base)[0] for a, b, base in jobs]
+    errors, got = [], {}
+
+    def worker(w):
+        try:
+            for rep in range(3):
+                for i, (a, b, base) in enumerate(jobs):
+                    if (i + w + rep) % 4:
+                        continue
+                    t, tn = ct.c_int(), ct.c_int()
+                    # three fields per mode in flight per context: a busy
+                    # context answers NICE_ERR_INVALID, retried
+                    for _ in range(100000):
+                        rc = lib.nice_detailed_submit(c._h, *N.api._split(a), *N.api._split(b), base, t)
+                        if rc != N._lib.NICE_ERR_INVALID:
+                            break
+                        time.sleep(0.0002)
+                    assert rc == 0, lib.nice_last_error()
+                    for _ in range(100000):
+                        rn = lib.nice_niceonly_submit(c._h, *N.api._split(a), *N.api._split(b), base,
+                                                      N.GpuContext._nice_opts(), tn)
+                        if rn != N._lib.NICE_ERR_INVALID:
+                            break
+                        time.sleep(0.0002)
+                    assert rn == 0, lib.nice_last_error()
+                    hist = (ct.c_uint64 * (base + 1))()
+                    cap = 1 << 14
+                    out = (N._lib.nice_number * cap)()
+                    n = ct.c_size_t()
+                    assert lib.nice_detailed_collect(c._h, t.value, hist, out, cap, n) == 0, lib.nice_last_error()
+                    det = (list(hist), [(out[q].number_lo | (out[q].number_hi << 64), out[q].num_uniques)
+                                        for q in range(n.value)])
+                    assert lib.nice_niceonly_collect(c._h, tn.value, out, cap, n, None) == 0
+                    nice = [out[q].number_lo | (out[q].number_hi << 64) for q in range(n.value)]
+                    got.setdefault(i, []).append((det, nice))
+        except BaseException as e:  # reported on the main thread
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(w,)) for w in range(4)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    c.close()
+    assert not errors, errors[0]
+    assert len(got) == len(jobs)
+    for i, results in got.items():
+        for det, nice in results:
+            assert det == want_det[i], jobs[i]
+            assert nice == want_nice[i], jobs[i]
