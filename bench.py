@@ -501,10 +501,10 @@ def main(args):
             line["roofline"]["hw_source"] = src
             line["roofline"]["hw_status"] = status
             if der is not None:
-                vb, lb = der.get("valu_busy"), der.get("lds_busy_timed", der.get("lds_busy"))
+                vb, lb = der.get("valu_busy"), der.get("lds_busy")
                 line["roofline"]["traffic"] = der.get("traffic_bytes")
                 line["roofline"]["hw"] = {
-                    "valu_busy": vb, "lds_busy": der.get("lds_busy"), "lds_busy_timed": lb,
+                    "valu_busy": vb, "lds_busy": lb,
                     "lds_conflict_frac": der.get("lds_conflict_frac"),
                     "lds_cycles_per_instr": der.get("lds_cycles_per_instr"),
                     "valu_lane_ops_per_n": der.get("valu_lane_ops_per_n"),
@@ -513,14 +513,15 @@ def main(args):
                     "note": "valu_busy = VALUBusy/100 (SQ_ACTIVE_INST_VALU / CUs / kernel cycles; it "
                             "can pass 1 with the fast-issue integer ops, profiles/r01/"
                             "isa_issue_rates_gfx950.log); lds_busy = SQ_LDS_IDX_ACTIVE / CUs / kernel "
-                            "cycles (the CU's one LDS pipe), which for this kernel's 8-byte reads "
-                            "overstates the LDS time ~2.3x: lds_busy_timed applies the s_memtime / "
-                            "counter ratio measured on the kernel's own index trace (profiles/r04/"
-                            "pmc_lds_trace.txt); lds_conflict_frac = SQ_LDS_BANK_CONFLICT / "
+                            "cycles (the CU's one LDS pipe; the counter matches the CU's s_memtime "
+                            "span on the kernel's own index trace, profiles/r04/lds_trace.log); "
+                            "both pipes near 1 = co-bound; lds_conflict_frac = SQ_LDS_BANK_CONFLICT / "
                             "SQ_LDS_IDX_ACTIVE; kernel cycles = GRBM_GUI_ACTIVE / XCDs"}
                 if vb is not None and lb is not None:
-                    pipe, busy = ("valu", vb) if vb >= lb else ("lds", lb)
-                    line["roofline"]["hw_bound"] = {"pipe": pipe, "busy": busy}
+                    (pipe, busy), other = sorted([("valu", vb), ("lds", lb)], key=lambda x: -x[1])
+                    line["roofline"]["hw_bound"] = {"pipe": pipe, "busy": busy,
+                                                    "other_pipe": other[0], "other_busy": other[1],
+                                                    "co_bound": other[1] >= 0.85}
                     line["roofline"]["frac_hw"] = busy
     st = last_stats[0]
     if st is not None:

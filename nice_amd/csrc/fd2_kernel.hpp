@@ -249,12 +249,11 @@ struct Cfg {
     // into X1, 8-byte entries of the digits 0..63 (ds_read_b64), and X2, 4-byte
     // entries of the digits 64.. (ds_read_b32), each table at its own entry
     // size, so both spread a lane group over all 64 banks: the stored limb
-    // (scaled by 8) addresses X1 directly and X2 after one shift.  On the
-    // kernel's own b80 index pattern b64 + b32 costs 3.9 LDS cycles per
-    // wave-lookup against 11.4 for one b128 of a 16-byte entry
-    // (scripts/ubench/lds_trace.hip, profiles/r04/lds_trace.log).  (Round 3's
-    // split kept X2 at an 8-byte stride, which puts a 32-lane group on half
-    // the banks: 26 % slower than the b128 layout in the kernel.)
+    // (scaled by 8) addresses X1 directly and X2 after one shift.  Probe
+    // only: on the kernel's own b80 index pattern b64 + b32 costs 11.9 LDS
+    // cycles per wave-lookup against 11.45 for one b128 of a 16-byte entry
+    // (scripts/ubench/lds_trace.hip, profiles/r04/lds_trace.log), and the
+    // kernel is 7 % slower with it.
     static constexpr bool SPLIT = MW == 3 && (VD_ & 512) != 0;
     static constexpr int ES = MW == 1 ? 4 : (MW == 2 || SPLIT ? 8 : 16);  // table entry stride (bytes)
     static constexpr int SH = T + ilog2(ES);                     // carry bit of a scaled limb

@@ -13,12 +13,11 @@ Per base (per-dispatch means over every fd2_kernel dispatch of the passes):
   bound               the busier pipe and its busy fraction
   lds_read            the table read of the base (ds_read_b64: 8-byte
                       entries, b40-64; ds_read_b128: 16-byte, b65-80)
-For ds_read_b64 the LDS counters report about 2.3-2.6x the cycles the reads
-take (scripts/ubench/lds_trace.hip on the kernel's own b40 / b80 index
-traces: counter 6.08 / 5.93 cycles per instruction, s_memtime 2.63 / 2.31,
-profiles/r04/pmc_lds_trace.txt, lds_trace.log); for ds_read_b128 they agree
-(11.4 both).  So lds_busy is an upper bound for b40-64 and a measurement for
-b65-80; lds_busy_timed scales the b64 bases' figure by the trace ratio.
+The LDS counter is a measurement for both reads: on the kernel's own b40 / b80
+index traces (scripts/ubench/lds_trace.hip) it reports 6.08 / 5.93 cycles per
+ds_read_b64 and 11.4 per ds_read_b128, and the CU's s_memtime span (first
+wave's start to last wave's end) gives 6.12 / 5.95 and 11.56 / 11.45
+(profiles/r04/pmc_lds_trace.txt, lds_trace.log).
 """
 import argparse
 import collections
@@ -29,7 +28,6 @@ import json
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-B64_COUNTER_OVER_TIMED = 6.08 / 2.63  # b40 trace (the b80 trace: 5.93 / 2.31)
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--out", required=True)
@@ -66,10 +64,9 @@ for b in a.bases:
     vb = m["VALUBusy"] / 100
     lb = m["SQ_LDS_IDX_ACTIVE"] / a.cus / cyc
     b128 = (b + 31) // 32 == 3
-    lbt = lb if b128 else lb / B64_COUNTER_OVER_TIMED
-    pipe, busy = ("valu", vb) if vb >= lbt else ("lds", lbt)
+    pipe, busy = ("valu", vb) if vb >= lb else ("lds", lb)
     res["bases"][str(b)] = {
-        "valu_busy": round(vb, 4), "lds_busy": round(lb, 4), "lds_busy_timed": round(lbt, 4),
+        "valu_busy": round(vb, 4), "lds_busy": round(lb, 4),
         "lds_conflict_frac": round(m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"], 4),
         "lds_cycles_per_instr": round(m["SQ_LDS_IDX_ACTIVE"] / m["SQ_INSTS_LDS"], 3),
         "valu_instr_per_wave_step": round(m["SQ_INSTS_VALU"] / ws, 2),

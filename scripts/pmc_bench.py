@@ -17,10 +17,9 @@ time).  Derived:
   lds_busy            SQ_LDS_IDX_ACTIVE / CUs / kernel_cycles: the share of the
                       kernel's cycles the CU's one LDS pipe is busy (the counter
                       aggregates the SIMDs of each SE)
-  lds_busy_timed      lds_busy scaled by the s_memtime / counter ratio of
-                      ds_read_b64 on the kernel's own index trace (2.63 / 6.08,
-                      profiles/r04/pmc_lds_trace.txt): the counters overstate
-                      the LDS cycles of 8-byte reads
+                      (the counter agrees with the CU's s_memtime span on the
+                      kernel's own index traces for ds_read_b64 and b128:
+                      scripts/ubench/lds_trace.hip, profiles/r04/lds_trace.log)
   lds_cycles_per_instr SQ_LDS_IDX_ACTIVE / SQ_INSTS_LDS (LDS cycles per wave64
                       LDS instruction; 4 is a conflict-free ds_read_b128)
   traffic_bytes       HBM bytes: FETCH_SIZE x 2 + WRITE_SIZE (KB -> B), separate passes
@@ -84,9 +83,6 @@ if "GRBM_GUI_ACTIVE" in mean:
     der["kernel_cycles"] = mean["GRBM_GUI_ACTIVE"] / a.xcds
     if "SQ_LDS_IDX_ACTIVE" in mean:
         der["lds_busy"] = mean["SQ_LDS_IDX_ACTIVE"] / a.cus / der["kernel_cycles"]
-        # the bench kernel (b40) reads 8-byte entries, for which the LDS
-        # counters report ~2.3x the cycles the reads take (scripts/pmc_bases.py)
-        der["lds_busy_timed"] = der["lds_busy"] / (6.08 / 2.63)
 if "SQ_LDS_IDX_ACTIVE" in mean and mean.get("SQ_INSTS_LDS"):
     der["lds_cycles_per_instr"] = mean["SQ_LDS_IDX_ACTIVE"] / mean["SQ_INSTS_LDS"]
 if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
