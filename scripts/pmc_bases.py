@@ -10,7 +10,8 @@ Per base (per-dispatch means over every fd2_kernel dispatch of the passes):
   lds_busy            SQ_LDS_IDX_ACTIVE / CUs / kernel cycles
   lds_conflict_frac   SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
   lds_cycles_per_instr SQ_LDS_IDX_ACTIVE / SQ_INSTS_LDS
-  bound               the busier pipe and its busy fraction
+  bound               the busier pipe and its busy fraction, the other pipe,
+                      and co_bound when the other is >= 0.85 busy too
   lds_read            the table read of the base (ds_read_b64: 8-byte
                       entries, b40-64; ds_read_b128: 16-byte, b65-80)
 The LDS counter is a measurement for both reads: on the kernel's own b40 / b80
@@ -64,7 +65,7 @@ for b in a.bases:
     vb = m["VALUBusy"] / 100
     lb = m["SQ_LDS_IDX_ACTIVE"] / a.cus / cyc
     b128 = (b + 31) // 32 == 3
-    pipe, busy = ("valu", vb) if vb >= lb else ("lds", lb)
+    (pipe, busy), (opipe, obusy) = sorted([("valu", vb), ("lds", lb)], key=lambda x: -x[1])
     res["bases"][str(b)] = {
         "valu_busy": round(vb, 4), "lds_busy": round(lb, 4),
         "lds_conflict_frac": round(m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"], 4),
@@ -72,7 +73,8 @@ for b in a.bases:
         "valu_instr_per_wave_step": round(m["SQ_INSTS_VALU"] / ws, 2),
         "lds_instr_per_wave_step": round(m["SQ_INSTS_LDS"] / ws, 2),
         "kernel_cycles": round(cyc), "lds_read": "ds_read_b128" if b128 else "ds_read_b64",
-        "bound": {"pipe": pipe, "busy": round(busy, 4)},
+        "bound": {"pipe": pipe, "busy": round(busy, 4), "other_pipe": opipe, "other_busy": round(obusy, 4),
+                  "co_bound": obusy >= 0.85},
         "dispatches": n, "files": [os.path.relpath(p, ROOT) for p in paths]}
     print(b, json.dumps({k: v for k, v in res["bases"][str(b)].items() if k not in ("files", "dispatches")}))
 with open(a.out, "w") as fh:
