@@ -170,6 +170,35 @@ constexpr int valu_limbs(int base) {
     }
 }
 
+// Fields of >= 1e7 on the three-mask-word bases (b65..80, the persistent
+// 1024-thread kernel, LDS-bound): limb 0 by VALU and the VALU-decoded C limbs
+// just BELOW the top stepped one (VD & 2048, Cfg::VDB).  The top stepped limb
+// only takes carries, so across a wave its lookup is nearly a broadcast (4 LDS
+// cycles on b80's index pattern against 11-12 for the limbs below it,
+// scripts/ubench/lds_trace_gen.py), and decoding it by VALU saved little;
+// decoding the limb below it instead saves a full-price lookup.  How many:
+// per limb layout (the segment's ND, NE), from interleaved A/B sweeps over
+// 1e9 fields at several points of each range (profiles/r04/vd_below_top.log):
+// b65 -3.6 / -5.5 %, b67 -2.4 / -3.7, b68 -3.5 / -2.3, b80 -1.8 .. -9.4 %.
+// The two-word bases (co-bound by VALU and LDS) move their VALU-decoded
+// limbs below the top where that measured faster at both points of the
+// range: b50 -1.1 / -2.2 %, b53 -1.1 / -1.4, b60 -1.2 / -1.7 (same VALU work,
+// cheaper lookups); elsewhere within +-1 % or mixed, unchanged.
+constexpr int valu_limbs_big(int base, int nd, int ne) {
+    if (base == 50 || base == 53 || base == 60) return valu_limbs(base) | 2048;
+    if ((base + 31) / 32 != 3) return valu_limbs(base);
+    if (base == 80) return 256 | 2048 | (nd == 8 && ne == 16 ? 3 : 2);
+    return 256 | 2048 | 1;
+}
+// b80's (ND 8, NE 16) layout spans the first ~40 % of the range, where the top
+// limb of 3n^2 (the one the top stepped C limb takes its carries from) grows
+// from ~1000 to B: below n = B80_E1_SMALL (top limb < 2000, the first 12 % of
+// the range, the hi-base benchmark field among them) the top C limb changes
+// rarely enough that one limb below it by VALU wins (6.66 vs 6.72 ms at the
+// range start), above it three (7.12 vs 7.47 ms at 0.25).
+constexpr unsigned __int128 B80_E1_SMALL =
+    ((unsigned __int128)0xb7761abcfull << 64) | 0x4b9a122bec71fdbbull;  // isqrt(2000 * 6400^15 / 3)
+
 // LDS bytes / waves per SIMD of a base's kernel at a workgroup size (the
 // formulas of Cfg, evaluated without instantiating it).
 constexpr int lds_bytes(int base, int wg) {
@@ -337,6 +366,14 @@ struct Cfg {
     // MW = 3) for one data-random (bank-conflicting) LDS read.
     static constexpr int VD = VD_;
     static constexpr int VDC = VD % 16, VDS = (VD / 16) % 16;
+    // VD & 2048 (b65..80 probe): the VALU-decoded limbs sit just BELOW the
+    // top stepped limb instead of at it.  The top stepped limb only takes
+    // carries, so its value is nearly the same in every lane of a wave and
+    // its lookup is nearly a broadcast (4 LDS cycles on b80's index pattern),
+    // while the limbs below it cost 11-12 (scripts/ubench/lds_trace_gen.py).
+    static constexpr int VDB = (VD & 2048) ? 1 : 0;
+    static constexpr bool vd_s(int q) { return q >= SL - VDB - VDS && q < SL - VDB; }
+    static constexpr bool vd_c(int q) { return q >= CL - VDB - VDC && q < CL - VDB; }
     // Lookup groups: a scheduling barrier after every LG table lookups of a
     // step (0: none), so the compiler cannot hoist all of a step's LDS reads
     // ahead of their ORs -- with SPLIT's b64 + u16 pairs that held ~75 VGPRs
@@ -363,7 +400,7 @@ struct Cfg {
     static constexpr bool VDL = (VD & 256) != 0 && !LSD;
     static constexpr u32 MAGIC_D = (u32)(((1ull << 32) + ES * BASE - 1) / (ES * BASE));
     static_assert(VD == 0 || (MW >= 2 && split_exact(BASE, ES, MAGIC_D)), "VALU digit split");
-    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1 && (VD & ~0x7ff) == 0 &&
+    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1 && (VD & ~0xfff) == 0 &&
                       ((VD & 1024) == 0 || LSDX),
                   "VALU-decoded limbs");
     // Waves per SIMD: what the LDS allows, capped by what the lane state
@@ -987,14 +1024,14 @@ __device__ __forceinline__ void walk_chunk(State<P> &st, const unsigned char *sm
 #pragma unroll
             for (int q = P::LO; q < P::SL; q++) {
                 if ((P::PROBE & 4) && q == 1) { m[0] |= st.S[q] & 0xffu; continue; }  // probe: no limb-1 lookups
-                if (q >= P::SL - P::VDS || (P::VDL && q == 0)) or_valu<P>(st.S[q] - P::EBT, m);
+                if (P::vd_s(q) || (P::VDL && q == 0)) or_valu<P>(st.S[q] - P::EBT, m);
                 else or_lookup<P, P::TB - (int)P::EBT, P::T2 - (int)P::EBT / 2>(smem, st.S[q], m);
                 if (P::LG && (q - P::LO + 1) % P::LG == 0) lookup_group_end<P>(m);
             }
 #pragma unroll
             for (int q = P::LO; q < P::CL; q++) {
                 if ((P::PROBE & 4) && q == 1) { m[1] |= st.C[q] & 0xffu; continue; }
-                if (q >= P::CL - P::VDC || (P::VDL && q == 0)) or_valu<P>(st.C[q], m);
+                if (P::vd_c(q) || (P::VDL && q == 0)) or_valu<P>(st.C[q], m);
                 else or_lookup<P, P::TB, P::T2>(smem, st.C[q], m);
                 if (P::LG && (P::SL + q - 2 * P::LO + 1) % P::LG == 0) lookup_group_end<P>(m);
             }

@@ -41,6 +41,25 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
         case 358: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 258>>(p, num_cus, s);
         default: break;
         }
+        // b65..80: VALU-decoded limbs just below the top stepped limb (VD &
+        // 2048): NICE_FD2_VD = 100 + VD as above
+        if constexpr ((B_ + 31) / 32 == 3) {
+            switch ((int)probe_knob("NICE_FD2_VD", 0)) {
+            case 2405: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 2305>>(p, num_cus, s);
+            case 2406: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 2306>>(p, num_cus, s);
+            case 2420: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 2320>>(p, num_cus, s);
+            case 2407: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 2307>>(p, num_cus, s);
+            case 2421: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 2321>>(p, num_cus, s);
+            case 2422: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 2322>>(p, num_cus, s);
+            default: break;
+            }
+        }
+        // Any base with VALU-decoded top limbs: the same count just below the
+        // top stepped limbs instead (VD & 2048): NICE_FD2_VD = 5000
+        if constexpr ((valu_limbs(B_) & 0xff) != 0 && (valu_limbs(B_) & 2048) == 0) {
+            if ((int)probe_knob("NICE_FD2_VD", 0) == 5000)
+                return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), valu_limbs(B_) | 2048>>(p, num_cus, s);
+        }
         // Low-digit table with a side table of carries (Cfg::LSDX, b59..64):
         // NICE_FD2_VD = 1100 + VD, VD = the VALU-decoded top limbs
         constexpr int DB_ = B_ - 32;
@@ -92,9 +111,15 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
 #endif
         // (the LSDX bases' tables leave room for one workgroup per CU: 1024
         // threads for every field size, 4 waves per SIMD instead of 2)
+        // (fields of >= 1e7 take valu_limbs_big: see there)
+        if constexpr (B_ == 80 && ND_ == 8 && NE_ == 16) {
+            if (!wg512 && (((unsigned __int128)p.start_hi << 64) | p.start_lo) < B80_E1_SMALL)
+                return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 256 | 2048 | 1>>(p, num_cus, s);
+        }
         constexpr bool small512 = (valu_limbs(B_) & 1024) == 0;
-        return wg512 && small512 ? launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, valu_limbs(B_)>>(p, num_cus, s)
-                                 : launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), valu_limbs(B_)>>(p, num_cus, s);
+        return wg512 && small512
+                   ? launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, valu_limbs(B_)>>(p, num_cus, s)
+                   : launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), valu_limbs_big(B_, ND_, NE_)>>(p, num_cus, s);
     }
 }
 
