@@ -488,6 +488,35 @@ def test_detailed_field_longer_than_one_launch(ctx, base, size):
     assert all(O.num_unique_digits(n, base) == u for n, u in l)
 
 
+# Where the per-layout VALU-decode choice of fields >= 1e7 (valu_limbs_big,
+# fd2_kernel.hpp) changes the kernel: b50/53/60 (below-top decode), b65/67/68
+# (limb 0 + one below the top), b80 on both sides of B80_E1_SMALL (12 % into
+# the range) and on the 17-limb layout (past ~40 %).
+BIG_VD_CASES = [(50, 0.0), (50, 0.6), (53, 0.3), (60, 0.0), (60, 0.7), (65, 0.0), (65, 0.5), (67, 0.4),
+                (68, 0.0), (68, 0.8), (80, 0.0), (80, 0.05), (80, 0.2), (80, 0.33), (80, 0.6), (80, 0.95)]
+
+
+@pytest.mark.parametrize("base,frac", BIG_VD_CASES)
+def test_big_field_valu_decode_variants(ctx, base, frac):
+    """A 2e7 field takes the >= 1e7 kernel (1024-thread persistent grid, its
+    valu_limbs_big choice); its four 5e6 quarters take the small-field
+    kernel (512 threads, the base's other VALU-decode choice), which the
+    oracle fuzz pins.  The histograms must add up and the near-miss lists
+    concatenate exactly, and every near-miss must recompute by the oracle."""
+    r0, r1 = O.base_range(base)
+    s = r0 + int((r1 - r0) * frac)
+    size, q = 2 * 10 ** 7, 5 * 10 ** 6
+    h, l = ctx.detailed_raw(s, s + size, base)
+    assert sum(h) == size
+    hs, ls = [0] * len(h), []
+    for k in range(4):
+        hk, lk = ctx.detailed_raw(s + k * q, s + (k + 1) * q, base)
+        hs = [a + b for a, b in zip(hs, hk)]
+        ls += lk
+    assert hs == h and ls == l, (base, frac)
+    assert all(O.num_unique_digits(n, base) == u for n, u in l)
+
+
 @pytest.mark.parametrize("where", MSD_WHERE)
 @pytest.mark.parametrize("chunk", [0, 10 ** 8])
 def test_niceonly_list_longer_than_device_capacity(ctx, where, chunk):
