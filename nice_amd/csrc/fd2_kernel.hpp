@@ -171,15 +171,18 @@ constexpr int valu_limbs(int base) {
 }
 
 // Fields of >= 1e7 on the three-mask-word bases (b65..80, the persistent
-// 1024-thread kernel, LDS-bound): limb 0 by VALU and the VALU-decoded C limbs
-// just BELOW the top stepped one (VD & 2048, Cfg::VDB).  The top stepped limb
-// only takes carries, so across a wave its lookup is nearly a broadcast (4 LDS
-// cycles on b80's index pattern against 11-12 for the limbs below it,
+// 1024-thread kernel): limb 0 by VALU and the VALU-decoded C limbs just BELOW
+// the top stepped one (VD & 2048, Cfg::VDB).  The top stepped limb only takes
+// carries, so across a wave its lookup is nearly a broadcast (4 LDS cycles on
+// b80's index pattern against 11-12 for the limbs below it,
 // scripts/ubench/lds_trace_gen.py), and decoding it by VALU saved little;
-// decoding the limb below it instead saves a full-price lookup.  How many:
-// per limb layout (the segment's ND, NE), from interleaved A/B sweeps over
-// 1e9 fields at several points of each range (profiles/r04/vd_below_top.log):
-// b65 -3.6 / -5.5 %, b67 -2.4 / -3.7, b68 -3.5 / -2.3, b80 -1.8 .. -9.4 %.
+// decoding the limbs below it saves full-price lookups.  How many: per limb
+// layout (the segment's ND, NE), from interleaved A/B sweeps over 1e9 fields
+// at several points of each range with the select-free decode of or_valu
+// (profiles/r04/vd_below_top.log): b65 2, b67 / b68 3, b80 3 (4 where n^3 has
+// 17 limbs).  Against the round-3 choice (top limbs / limb 0 only): b80 1e9
+// 6.84 -> 6.43 ms at the range start, b65 5.97 -> 5.52, b67 5.94 -> 5.69,
+// b68 6.48 -> 5.85.
 // The two-word bases (co-bound by VALU and LDS) move their VALU-decoded
 // limbs below the top where that measured faster at both points of the
 // range: b50 -1.1 / -2.2 %, b53 -1.1 / -1.4, b60 -1.2 / -1.7 (same VALU work,
@@ -187,17 +190,10 @@ constexpr int valu_limbs(int base) {
 constexpr int valu_limbs_big(int base, int nd, int ne) {
     if (base == 50 || base == 53 || base == 60) return valu_limbs(base) | 2048;
     if ((base + 31) / 32 != 3) return valu_limbs(base);
-    if (base == 80) return 256 | 2048 | (nd == 8 && ne == 16 ? 3 : 2);
-    return 256 | 2048 | 1;
+    if (base == 65) return 256 | 2048 | 2;
+    if (base == 80 && ne == 17) return 256 | 2048 | 4;
+    return 256 | 2048 | 3;
 }
-// b80's (ND 8, NE 16) layout spans the first ~40 % of the range, where the top
-// limb of 3n^2 (the one the top stepped C limb takes its carries from) grows
-// from ~1000 to B: below n = B80_E1_SMALL (top limb < 2000, the first 12 % of
-// the range, the hi-base benchmark field among them) the top C limb changes
-// rarely enough that one limb below it by VALU wins (6.66 vs 6.72 ms at the
-// range start), above it three (7.12 vs 7.47 ms at 0.25).
-constexpr unsigned __int128 B80_E1_SMALL =
-    ((unsigned __int128)0xb7761abcfull << 64) | 0x4b9a122bec71fdbbull;  // isqrt(2000 * 6400^15 / 3)
 
 // LDS bytes / waves per SIMD of a base's kernel at a workgroup size (the
 // formulas of Cfg, evaluated without instantiating it).
@@ -507,11 +503,16 @@ __device__ __forceinline__ void or_valu(u32 vs, u32 (&m)[P::MW]) {
         m[0] |= (u32)bits;
         m[1] |= (u32)(bits >> 32);
     } else {
+        // Digit d < 96 without compares or selects: a 64-bit shift by d
+        // (the hardware takes d mod 64) is right in words 0 and 1 for d < 64,
+        // and for d >= 64 leaves bit d - 64 in word 0 and nothing in word 1;
+        // word 2's bit is bit 6 of d shifted by d mod 32, which is exactly that
+        // stray bit, so XOR-ing it out of word 0 leaves every word right.
         const u64 bq = 1ull << (q & 63), br = 1ull << (r & 63);
-        const u64 lo = (q < 64 ? bq : 0ull) | (r < 64 ? br : 0ull);
-        m[0] |= (u32)lo;
-        m[1] |= (u32)(lo >> 32);
-        m[2] |= (q >= 64 ? (u32)bq : 0u) | (r >= 64 ? (u32)br : 0u);
+        const u32 wq = __builtin_amdgcn_ubfe(q, 6, 1) << (q & 31), wr = __builtin_amdgcn_ubfe(r, 6, 1) << (r & 31);
+        m[0] |= ((u32)bq ^ wq) | ((u32)br ^ wr);
+        m[1] |= (u32)(bq >> 32) | (u32)(br >> 32);
+        m[2] |= wq | wr;
     }
 }
 

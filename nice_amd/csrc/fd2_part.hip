@@ -51,6 +51,8 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
             case 2407: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 2307>>(p, num_cus, s);
             case 2421: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 2321>>(p, num_cus, s);
             case 2422: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 2322>>(p, num_cus, s);
+            case 2408: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 2308>>(p, num_cus, s);
+            case 2423: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 2323>>(p, num_cus, s);
             default: break;
             }
         }
@@ -112,10 +114,6 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
         // (the LSDX bases' tables leave room for one workgroup per CU: 1024
         // threads for every field size, 4 waves per SIMD instead of 2)
         // (fields of >= 1e7 take valu_limbs_big: see there)
-        if constexpr (B_ == 80 && ND_ == 8 && NE_ == 16) {
-            if (!wg512 && (((unsigned __int128)p.start_hi << 64) | p.start_lo) < B80_E1_SMALL)
-                return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), 256 | 2048 | 1>>(p, num_cus, s);
-        }
         constexpr bool small512 = (valu_limbs(B_) & 1024) == 0;
         return wg512 && small512
                    ? launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, valu_limbs(B_)>>(p, num_cus, s)
