@@ -178,11 +178,10 @@ constexpr int valu_limbs(int base) {
 // scripts/ubench/lds_trace_gen.py), and decoding it by VALU saved little;
 // decoding the limbs below it saves full-price lookups.  How many: per limb
 // layout (the segment's ND, NE), from interleaved A/B sweeps over 1e9 fields
-// at several points of each range with the select-free decode of or_valu
-// (profiles/r04/vd_below_top.log): b65 2, b67 / b68 3, b80 3 (4 where n^3 has
-// 17 limbs).  Against the round-3 choice (top limbs / limb 0 only): b80 1e9
-// 6.84 -> 6.43 ms at the range start, b65 5.97 -> 5.52, b67 5.94 -> 5.69,
-// b68 6.48 -> 5.85.
+// at several points of each range with the select-free decode of or_valu and
+// the one-multiply C carry (profiles/r04/vd_below_top.log): three, four where
+// b80's n^3 has 17 limbs.  Against the round-3 kernels: b80 1e9 6.84 -> 6.24
+// ms at the range start, b65 5.97 -> 5.43, b67 5.94 -> 5.64, b68 6.48 -> 5.57.
 // The two-word bases (co-bound by VALU and LDS) move their VALU-decoded
 // limbs below the top where that measured faster at both points of the
 // range: b50 -1.1 / -2.2 %, b53 -1.1 / -1.4, b60 -1.2 / -1.7 (same VALU work,
@@ -190,7 +189,6 @@ constexpr int valu_limbs(int base) {
 constexpr int valu_limbs_big(int base, int nd, int ne) {
     if (base == 50 || base == 53 || base == 60) return valu_limbs(base) | 2048;
     if ((base + 31) / 32 != 3) return valu_limbs(base);
-    if (base == 65) return 256 | 2048 | 2;
     if (base == 80 && ne == 17) return 256 | 2048 | 4;
     return 256 | 2048 | 3;
 }
@@ -351,9 +349,13 @@ struct Cfg {
     static constexpr u32 DC = ES * B;
     static constexpr u32 MAGIC = (u32)(((1ull << 32) + DC - 1) / DC);
     static constexpr unsigned long long TMAX = (unsigned long long)ES * (5ull * B + 4);
-    // Where one multiply-high by ceil(2^32 / (ES B)) is not exact over
-    // [0, TMAX] (b80: ES = 16), divide t / ES first (t is a multiple of ES).
-    static constexpr bool C1 = ((unsigned long long)MAGIC * DC - (1ull << 32)) * TMAX < (1ull << 32);
+    // One multiply-high by MAGIC is exact because t is a multiple of ES:
+    // with t = ES u, u = qB + r and ES B MAGIC = 2^32 + e, the product is
+    // q + r / B + u e / (B 2^32), whose floor is q while u e < 2^32 (b80:
+    // u <= 5B + 4 = 32004, e = 98304).  Where even that fails, divide t / ES
+    // first.  (Rounds 1-3 bounded t e < 2^32 instead, which sent the
+    // 16-byte-entry bases b65..80 down the extra shift per C limb.)
+    static constexpr bool C1 = ((unsigned long long)MAGIC * DC - (1ull << 32)) * (TMAX / ES) < (1ull << 32);
     static constexpr u32 MAGICB = (u32)(((1ull << 32) + B - 1) / B);
     // VALU-decoded limbs (no table lookup): VD % 16 of the top stepped C
     // limbs and VD / 16 of the top stepped S limbs.  Their two digits come
