@@ -95,18 +95,17 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
         default: break;
         }
         // Lookup-group sweep of the three-mask-word bases (NICE_FD2_LG = LG,
-        // or 1000 + LG: the split b64 + u16 layout with that grouping)
+        // at the production VALU-decoded limbs of fields >= 1e7)
         if constexpr ((B_ + 31) / 32 == 3) {
-            constexpr int VL = valu_limbs(B_), WGB = big_wg(B_);
+            constexpr int VL = valu_limbs_big(B_, ND_, NE_), WGB = big_wg(B_);
             switch ((int)probe_knob("NICE_FD2_LG", 100000)) {
             case 0: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL, 0>>(p, num_cus, s);
+            case 5: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL, 5>>(p, num_cus, s);
             case 6: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL, 6>>(p, num_cus, s);
+            case 7: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL, 7>>(p, num_cus, s);
             case 8: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL, 8>>(p, num_cus, s);
+            case 10: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL, 10>>(p, num_cus, s);
             case 12: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL, 12>>(p, num_cus, s);
-            case 16: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL, 16>>(p, num_cus, s);
-            case 1000: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL | 512, 0>>(p, num_cus, s);
-            case 1008: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL | 512, 8>>(p, num_cus, s);
-            case 1012: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, WGB, VL | 512, 12>>(p, num_cus, s);
             default: break;
             }
         }
