@@ -185,8 +185,14 @@ constexpr int valu_limbs(int base) {
 // The two-word bases (co-bound by VALU and LDS) move their VALU-decoded
 // limbs below the top where that measured faster at both points of the
 // range: b50 -1.1 / -2.2 %, b53 -1.1 / -1.4, b60 -1.2 / -1.7 (same VALU work,
-// cheaper lookups); elsewhere within +-1 % or mixed, unchanged.
+// cheaper lookups); elsewhere within +-1 % or mixed, unchanged.  b40 (no
+// VALU-decoded limbs before) decodes one C limb below the top on its 8-limb
+// n^3 layouts (the first ~45 % of the range, the extra-large benchmark field
+// among them): 2.03 -> 1.98 ms at the range start, 2.74 -> 2.62 at 0.1, 2.22
+// -> 2.17 at 0.3; on the 9-limb layout it lost 0-2 % and stays as it was
+// (profiles/r04/vd_b40.log).
 constexpr int valu_limbs_big(int base, int nd, int ne) {
+    if (base == 40) return ne == 8 ? 2048 | 1 : 0;
     if (base == 50 || base == 53 || base == 60) return valu_limbs(base) | 2048;
     if ((base + 31) / 32 != 3) return valu_limbs(base);
     if (base == 80 && ne == 17) return 256 | 2048 | 4;

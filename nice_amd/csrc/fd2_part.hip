@@ -56,6 +56,18 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
             default: break;
             }
         }
+        // Two-word bases: k limbs below the top stepped ones by VALU (VD & 2048,
+        // keeping the base's low-digit-table mode): NICE_FD2_VD = 6000 + k
+        if constexpr ((B_ + 31) / 32 == 2) {
+            constexpr int KEEP = valu_limbs(B_) & 1024;
+            switch ((int)probe_knob("NICE_FD2_VD", 0)) {
+            case 6001: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), KEEP | 2048 | 1>>(p, num_cus, s);
+            case 6002: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), KEEP | 2048 | 2>>(p, num_cus, s);
+            case 6003: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), KEEP | 2048 | 3>>(p, num_cus, s);
+            case 6017: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), KEEP | 2048 | 17>>(p, num_cus, s);
+            default: break;
+            }
+        }
         // Any base with VALU-decoded top limbs: the same count just below the
         // top stepped limbs instead (VD & 2048): NICE_FD2_VD = 5000
         if constexpr ((valu_limbs(B_) & 0xff) != 0 && (valu_limbs(B_) & 2048) == 0) {

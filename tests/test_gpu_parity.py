@@ -489,10 +489,11 @@ def test_detailed_field_longer_than_one_launch(ctx, base, size):
 
 
 # Where the per-layout VALU-decode choice of fields >= 1e7 (valu_limbs_big,
-# fd2_kernel.hpp) changes the kernel: b50/53/60 (below-top decode), b65/67/68
+# fd2_kernel.hpp) changes the kernel: b40 on its 8-limb n^3 layouts and
+# b50/53/60 (below-top decode), b65/67/68
 # (limb 0 + two / three below the top), b80 on its 16-limb layouts (the first
 # ~40 % of the range) and on the 17-limb one (four below the top).
-BIG_VD_CASES = [(50, 0.0), (50, 0.6), (53, 0.3), (60, 0.0), (60, 0.7), (65, 0.0), (65, 0.5), (67, 0.4),
+BIG_VD_CASES = [(40, 0.0), (40, 0.1), (40, 0.35), (40, 0.7), (50, 0.0), (50, 0.6), (53, 0.3), (60, 0.0), (60, 0.7), (65, 0.0), (65, 0.5), (67, 0.4),
                 (68, 0.0), (68, 0.8), (80, 0.0), (80, 0.05), (80, 0.2), (80, 0.33), (80, 0.6), (80, 0.95)]
 
 
