@@ -442,6 +442,16 @@ __device__ __forceinline__ u32 mad_u24(u32 a, u32 c) {
     return r;
 }
 
+// v_mad_i32_i24 with a scalar multiplier: a * K + c on 24-bit signed a, K
+// (LLVM otherwise turns c - a * K into a v_mad_u64_u32, which does not issue
+// at the full rate).
+template <int K>
+__device__ __forceinline__ u32 mad_i24s(u32 a, u32 c) {
+    u32 r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(K), "v"(c));
+    return r;
+}
+
 // v_bcnt_u32_b32 with a scalar accumulator: popcount(x) + acc.
 __device__ __forceinline__ u32 bcnt_acc(u32 x, u32 acc) {
     u32 r;
@@ -505,7 +515,7 @@ __device__ __forceinline__ void lookup_group_end(u32 (&m)[P::MW]) {
 template <class P>
 __device__ __forceinline__ void or_valu(u32 vs, u32 (&m)[P::MW]) {
     const u32 q = __umulhi(vs, P::MAGIC_D);                        // high digit
-    const u32 r = vs / (u32)P::ES - q * (u32)P::BASE;             // low digit
+    const u32 r = mad_i24s<-P::BASE>(q, vs / (u32)P::ES);          // low digit
     if constexpr (P::MW == 2) {
         const u64 bits = (1ull << q) | (1ull << r);
         m[0] |= (u32)bits;
