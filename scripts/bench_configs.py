@@ -46,6 +46,13 @@ def main():
     a = ap.parse_args()
     ctx = N.GpuContext(0)
     out = []
+    # Warm the GPU up before the first timed config: the first fields after
+    # an idle spell run ~5 % slow (clocks ramping; profiles/r04/
+    # vd_below_top_order.log), which would charge the first row.
+    w = get_benchmark_field(BM.EXTRA_LARGE)
+    t_end = time.perf_counter() + 0.5
+    while time.perf_counter() < t_end:
+        ctx.detailed_raw(w.range_start, w.range_end, w.base)
 
     def det(name, f, note=""):
         sec, (hist, lst) = timed(lambda: ctx.detailed_raw(f.range_start, f.range_end, f.base), a.reps)
