@@ -189,8 +189,9 @@ constexpr int valu_limbs(int base) {
 // VALU-decoded limbs before) decodes one C limb below the top on its 8-limb
 // n^3 layouts (the first ~45 % of the range, the extra-large benchmark field
 // among them): 2.03 -> 1.98 ms at the range start, 2.74 -> 2.62 at 0.1, 2.22
-// -> 2.17 at 0.3; on the 9-limb layout it lost 0-2 % and stays as it was
-// (profiles/r04/vd_b40.log).
+// -> 2.17 at 0.3, and it beats one or two more decoded limbs at every point
+// checked in 0.02..0.35; on the 9-limb layout it lost 0-2 % and stays as it
+// was (profiles/r04/vd_b40.log).
 constexpr int valu_limbs_big(int base, int nd, int ne) {
     if (base == 40) return ne == 8 ? 2048 | 1 : 0;
     if (base == 50 || base == 53 || base == 60) return valu_limbs(base) | 2048;
