@@ -37,6 +37,9 @@ extern "C" {
 #define NICE_ERR_NO_DEVICE 4   /* no usable GPU */
 #define NICE_ERR_MSD_OVERFLOW 5 /* device MSD work queues overflowed (msd_floor too small for
                                    chunk_size); not retryable with a larger list */
+#define NICE_ERR_BUSY 6         /* *_submit: every slot of the context holds a field in flight;
+                                   collect one and submit again (the synchronous calls wait
+                                   for a slot instead, see nice_process_range_detailed) */
 
 /* NiceNumberSimple (common/src/lib.rs:182-186). */
 typedef struct {
@@ -65,7 +68,14 @@ const char *nice_last_error(void);
  * (client_process_gpu.rs:812-897; CPU semantics client_process.rs:150-191).
  * hist receives base+1 u64 counts indexed by num_uniques (bin 0 is always 0;
  * FieldResults.distribution is bins 1..=base).  out receives the near-misses
- * (num_uniques > floor(base * 0.9f)) in ascending order of number. */
+ * (num_uniques > floor(base * 0.9f)) in ascending order of number.
+ * Thread-safe on a shared context (the reference shares its GpuContext across
+ * the client's tasks behind a Mutex, client/src/main.rs:622,
+ * client_process_gpu.rs:199-200): when every slot holds a field in flight the
+ * call blocks until another thread's collect frees one.  It returns
+ * NICE_ERR_BUSY instead only when no other thread could free a slot (every
+ * field in flight was submitted by the calling thread and is not being
+ * collected), which would otherwise deadlock. */
 int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi,
                                 uint64_t end_lo, uint64_t end_hi, uint32_t base,
                                 uint64_t *hist, nice_number *out, size_t cap, size_t *n_out);
@@ -86,7 +96,10 @@ int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start
  *              nice list is unchanged.
  *   chunk_size MSD chunking of the field; 0 -> reference client rule
  *              1e6 * clamp(ceil(size / 1e11), 1, 1000) (client/src/main.rs:158-168)
- *   threads    host MSD worker threads; 0 -> hardware concurrency
+ *   threads    host MSD worker threads; 0 -> available parallelism (the
+ *              affinity mask capped by the cgroup cpu.max quota, as Rust's
+ *              std::thread::available_parallelism, client_process_gpu.rs:598;
+ *              nice_host_threads)
  *   stride_k   LSD digits in the stride table; 0 -> 2 (client/src/main.rs:19)
  *   msd_where  where the MSD recursion runs: 0 auto (device for stride_k 2),
  *              1 host worker threads, 2 device (level-synchronous kernels)
@@ -122,9 +135,12 @@ typedef struct {
     uint32_t square_ok;     /* device MSD, in-range fast bases: candidates whose square alone
                                has no repeated digit (get_is_nice reached the cube scan),
                                mod 2^32; 0 where not counted (host MSD, other bases) */
-    double msd_seconds;     /* until the last MSD worker finished */
+    double msd_seconds;     /* until the last MSD worker finished (a field re-run after a
+                               list overflow: its last run) */
     double total_seconds;
     uint64_t msd_floor;     /* the MSD recursion floor this field used */
+    uint32_t msd_threads;   /* host MSD worker threads the field ran (0: device MSD) */
+    uint32_t reruns;        /* times the field re-ran with grown device lists */
 } nice_niceonly_stats;
 
 /* AdaptiveFloor::update's step (client_process_gpu.rs:130-157): the floor
@@ -222,6 +238,10 @@ int nice_last_kernel_stats(nice_ctx *ctx, int device_index, nice_kernel_stats *o
 int nice_ctx_set_kernel_timing(nice_ctx *ctx, int enable);
 
 /* Host helpers mirroring the reference functions the client calls. */
+/* std::thread::available_parallelism() (client_process_gpu.rs:598): the
+ * process's CPU affinity mask, capped by a cgroup v2 cpu.max quota.  The
+ * host MSD pool's size when nice_niceonly_opts.threads is 0. */
+uint32_t nice_host_threads(void);
 /* get_base_range_u128 (base_range.rs:43-54): 1 range, 0 none, -1 exceeds u128. */
 int nice_base_range(uint32_t base, uint64_t *start_lo, uint64_t *start_hi, uint64_t *end_lo,
                     uint64_t *end_hi);

@@ -21,6 +21,7 @@ NICE_ERR_HIP = 2
 NICE_ERR_CAPACITY = 3
 NICE_ERR_NO_DEVICE = 4
 NICE_ERR_MSD_OVERFLOW = 5
+NICE_ERR_BUSY = 6  # *_submit: every slot of the context is in flight
 NICE_MSD_FLOOR_ADAPTIVE = (1 << 64) - 1  # msd_floor: the reference GPU path's AdaptiveFloor
 
 # Every symbol include/nice_hip.h declares (checked by tests/test_abi.py).
@@ -36,6 +37,7 @@ EXPORTS = (
     "nice_detailed_collect", "nice_niceonly_submit", "nice_niceonly_collect",
     "nice_cpu_process_range_detailed", "nice_cpu_process_range_niceonly",
     "nice_adaptive_floor_step", "nice_adaptive_floor", "nice_ctx_set_kernel_timing",
+    "nice_host_threads",
 )
 
 
@@ -65,7 +67,8 @@ class nice_niceonly_stats(ctypes.Structure):
     _fields_ = [("ranges", ctypes.c_uint64), ("range_numbers", ctypes.c_uint64),
                 ("candidates", ctypes.c_uint64), ("launches", ctypes.c_uint32),
                 ("square_ok", ctypes.c_uint32), ("msd_seconds", ctypes.c_double),
-                ("total_seconds", ctypes.c_double), ("msd_floor", ctypes.c_uint64)]
+                ("total_seconds", ctypes.c_double), ("msd_floor", ctypes.c_uint64),
+                ("msd_threads", ctypes.c_uint32), ("reruns", ctypes.c_uint32)]
 
 
 class nice_kernel_stats(ctypes.Structure):
@@ -138,6 +141,7 @@ def lib():
         "nice_cpu_process_range_niceonly": ([u64, u64, u64, u64, u32, u32, i32, PN, sz, PSZ], i32),
         "nice_adaptive_floor_step": ([ctypes.c_double, ctypes.c_double, ctypes.c_double], ctypes.c_double),
         "nice_adaptive_floor": ([ctypes.POINTER(ctypes.c_double), P32], i32),
+        "nice_host_threads": ([], u32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -114,11 +114,23 @@ class NiceonlyStats:
     # the MSD recursion floor the field used (msd_floor="adaptive": the
     # adaptive floor's value at submit)
     msd_floor: int = 0
+    # host MSD worker threads the field ran (0: the MSD ran on the device)
+    msd_threads: int = 0
+    # times the field re-ran with grown device lists
+    reruns: int = 0
 
 
 def _stats(st) -> NiceonlyStats:
     return NiceonlyStats(st.ranges, st.range_numbers, st.candidates, st.launches,
-                         st.msd_seconds, st.total_seconds, st.square_ok, st.msd_floor)
+                         st.msd_seconds, st.total_seconds, st.square_ok, st.msd_floor,
+                         st.msd_threads, st.reruns)
+
+
+def host_threads() -> int:
+    """std::thread::available_parallelism() as the library computes it (the
+    affinity mask capped by the cgroup cpu.max quota): the host MSD pool's
+    size when threads=0 (client_process_gpu.rs:598)."""
+    return int(lib().nice_host_threads())
 
 
 def adaptive_floor_step(floor: float, msd_seconds: float, total_seconds: float) -> float:

@@ -207,6 +207,7 @@ struct Entry {
 struct DetJob {
     bool active = false, collected = false;
     bool waiting = false;          // a collect is waiting for it outside the context lock
+    std::thread::id owner;         // the submitting thread (acquire_slot's deadlock test)
     u128 s = 0, e = 0;
     uint32_t base = 0;
     std::vector<u128> bounds;      // per-device shard bounds
@@ -216,6 +217,7 @@ struct DetJob {
 struct NiceJob {
     bool active = false, collected = false;
     bool waiting = false;          // a collect is waiting for it outside the context lock
+    std::thread::id owner;         // the submitting thread (acquire_slot's deadlock test)
     // the submitted field, kept so that collect can re-run it (list overflow)
     u128 s = 0, e = 0;
     uint32_t base = 0;
@@ -236,6 +238,7 @@ struct NiceJob {
 struct nice_ctx {
     std::vector<Device> devs;
     std::mutex mu;  // serialises calls on one context (client_process_gpu.rs:196-201)
+    std::condition_variable freed;  // a collect released a slot (synchronous submits wait on it)
     bool timing = true;  // record HIP events around each detailed field (nice_ctx_set_kernel_timing)
     DetJob det[kSlots];
     NiceJob nice[kSlots];
@@ -255,6 +258,32 @@ int free_slot(const Job *jobs, int next) {
         if (!jobs[t].active) return t;
     }
     return -1;
+}
+
+// A free slot for a new field, under ctx->mu (held by `lock`).  Without
+// `wait`, NICE_ERR_BUSY when every slot is in flight (the asynchronous
+// submits: the caller collects one first).  With `wait` (the synchronous
+// reference-shaped calls, which the reference serves behind the context's
+// Mutex, client_process_gpu.rs:199-200), block until another thread's
+// collect frees one -- unless no other thread can: every field in flight was
+// submitted by this thread and nobody is collecting it.
+template <class Job>
+int acquire_slot(nice_ctx *ctx, std::unique_lock<std::mutex> &lock, const Job *jobs, int next, bool wait,
+                 const char *mode, int *slot) {
+    for (;;) {
+        const int t = free_slot(jobs, next);
+        if (t >= 0) {
+            *slot = t;
+            return NICE_OK;
+        }
+        bool others = false;
+        for (int i = 0; i < slots_used(); i++)
+            others |= jobs[i].active && (jobs[i].waiting || jobs[i].owner != std::this_thread::get_id());
+        if (!wait || !others)
+            return fail(NICE_ERR_BUSY, std::string("three ") + mode +
+                                           " fields already in flight on this context; collect one first");
+        ctx->freed.wait(lock);
+    }
 }
 
 int ensure_listbuf(Device &d, ListBuf &l, uint32_t cap, bool with_u) {
@@ -536,12 +565,22 @@ inline hipEvent_t done_event(const Slot &sl) {
 
 // Polls spin for the first kSpinPolls (a small field ends within tens of
 // microseconds, and a sleeping waiter would add its wake-up latency), then
-// yield the core between polls.
-constexpr uint32_t kSpinPolls = 1u << 14;
+// yield the core between polls for kYieldPolls more, then sleep between
+// polls, 20 us doubling to 200 us: a multi-second field (a split-launch
+// detailed field, the massive niceonly field) must not keep a core busy per
+// waiting thread beside the host MSD pool.  The sleep adds at most 200 us to
+// fields that run for milliseconds.
+constexpr uint32_t kSpinPolls = 1u << 14, kYieldPolls = 1u << 11;
 
 inline void backoff(uint32_t i) {
-    if (i < kSpinPolls) __builtin_ia32_pause();
-    else sched_yield();
+    if (i < kSpinPolls) {
+        __builtin_ia32_pause();
+    } else if (i < kSpinPolls + kYieldPolls) {
+        sched_yield();
+    } else {
+        const uint32_t k = std::min<uint32_t>((i - kSpinPolls - kYieldPolls) / 8, 3);
+        std::this_thread::sleep_for(std::chrono::microseconds(std::min(200u, 20u << (2 * k))));
+    }
 }
 
 // Wait for an event by polling it (see backoff).
@@ -643,10 +682,10 @@ int enqueue_detailed_shard(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, b
     return NICE_OK;
 }
 
-int detailed_submit(nice_ctx *ctx, u128 s, u128 e, uint32_t base, int *ticket) {
-    const int t = free_slot(ctx->det, ctx->det_next);
-    if (t < 0)
-        return fail(NICE_ERR_INVALID, "three detailed fields already in flight on this context; collect one first");
+int detailed_submit(nice_ctx *ctx, std::unique_lock<std::mutex> &lock, u128 s, u128 e, uint32_t base,
+                    bool wait, int *ticket) {
+    int t = -1;
+    if (int rc = acquire_slot(ctx, lock, ctx->det, ctx->det_next, wait, "detailed", &t)) return rc;
     DetJob &job = ctx->det[t];
     const size_t nd = ctx->devs.size();
     const u128 size = e - s;
@@ -661,6 +700,7 @@ int detailed_submit(nice_ctx *ctx, u128 s, u128 e, uint32_t base, int *ticket) {
     }
     job.active = true;
     job.collected = false;
+    job.owner = std::this_thread::get_id();
     job.s = s;
     job.e = e;
     job.base = base;
@@ -676,7 +716,9 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
     const size_t nd = ctx->devs.size();
     job.total.assign(base + 1, 0);
     job.all.clear();
+    std::vector<size_t> off(nd + 1, 0);  // device i's list entries: job.all[off[i], off[i + 1])
     for (size_t i = 0; i < nd; i++) {
+        off[i] = job.all.size();
         Device &d = ctx->devs[i];
         Slot &sl = d.slot[t];
         d.last = nice_kernel_stats{};
@@ -717,6 +759,7 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
             for (uint32_t q = 0; q < cnt; q++) job.all.push_back({mk(nbuf[2 * q], nbuf[2 * q + 1]), ubuf[q]});
         }
     }
+    off[nd] = job.all.size();
     // Self-check: the server's submit invariants (api/src/main.rs:309-359)
     // before anything is returned.
     int rc = validate_detailed(base, job.e - job.s, job.total.data(), job.all.size(),
@@ -725,41 +768,53 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
     if (!job.all.empty()) {
         // ... and its last one: every listed number's unique count recomputed
         // by the generic per-n device function (full square / cube + digit
-        // scan, a different code path from the FD kernel that listed it), on
-        // the auxiliary stream so no queued field is waited for.
-        Device &d = ctx->devs[0];
-        HIPCHK(hipSetDevice(d.id));
-        // created on first use: an idle stream would still take one of the
-        // process's few hardware queues (GPU_MAX_HW_QUEUES)
-        if (!d.aux) HIPCHK(hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking));
-        const size_t n = job.all.size();
-        std::vector<uint64_t> pairs(2 * n);
-        for (size_t i = 0; i < n; i++) {
-            pairs[2 * i] = lo64(job.all[i].n);
-            pairs[2 * i + 1] = hi64(job.all[i].n);
+        // scan, a different code path from the FD kernel that listed it).
+        // Each device recomputes its own shard's entries on its auxiliary
+        // stream (so no queued field is waited for), all devices at once.
+        std::vector<std::vector<uint32_t>> u(nd);
+        std::vector<std::vector<uint64_t>> pairs(nd);
+        for (size_t i = 0; i < nd; i++) {
+            const size_t n = off[i + 1] - off[i];
+            if (!n) continue;
+            Device &d = ctx->devs[i];
+            HIPCHK(hipSetDevice(d.id));
+            // created on first use: an idle stream would still take one of the
+            // process's few hardware queues (GPU_MAX_HW_QUEUES)
+            if (!d.aux) HIPCHK(hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking));
+            pairs[i].resize(2 * n);
+            for (size_t q = 0; q < n; q++) {
+                pairs[i][2 * q] = lo64(job.all[off[i] + q].n);
+                pairs[i][2 * q + 1] = hi64(job.all[off[i] + q].n);
+            }
+            if (d.chk_cap < n) {
+                // grown rarely (the recompute of the previous field finished
+                // before its collect returned, so nothing reads the old buffers)
+                if (d.chk_n) HIPCHK(hipFree(d.chk_n));
+                if (d.chk_u) HIPCHK(hipFree(d.chk_u));
+                d.chk_n = nullptr;
+                d.chk_u = nullptr;
+                d.chk_cap = 0;
+                const size_t c = std::max<size_t>(n, 4096);
+                HIPCHK(hipMalloc(&d.chk_n, c * 16));
+                HIPCHK(hipMalloc(&d.chk_u, c * 4));
+                d.chk_cap = c;
+            }
+            u[i].resize(n);
+            hipError_t err = hipMemcpyAsync(d.chk_n, pairs[i].data(), n * 16, hipMemcpyHostToDevice, d.aux);
+            if (err == hipSuccess) err = nice::launch_unique_counts(d.chk_n, (uint32_t)n, base, d.chk_u, d.aux);
+            if (err == hipSuccess) err = hipMemcpyAsync(u[i].data(), d.chk_u, n * 4, hipMemcpyDeviceToHost, d.aux);
+            if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("self-check: ") + hipGetErrorString(err));
         }
-        if (d.chk_cap < n) {
-            // grown rarely (the recompute of the previous field finished
-            // before its collect returned, so nothing reads the old buffers)
-            if (d.chk_n) HIPCHK(hipFree(d.chk_n));
-            if (d.chk_u) HIPCHK(hipFree(d.chk_u));
-            d.chk_n = nullptr;
-            d.chk_u = nullptr;
-            d.chk_cap = 0;
-            const size_t c = std::max<size_t>(n, 4096);
-            HIPCHK(hipMalloc(&d.chk_n, c * 16));
-            HIPCHK(hipMalloc(&d.chk_u, c * 4));
-            d.chk_cap = c;
+        for (size_t i = 0; i < nd; i++) {
+            if (u[i].empty()) continue;
+            Device &d = ctx->devs[i];
+            HIPCHK(hipSetDevice(d.id));
+            const hipError_t err = hipStreamSynchronize(d.aux);
+            if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("self-check: ") + hipGetErrorString(err));
+            for (size_t q = 0; q < u[i].size(); q++)
+                if (u[i][q] != job.all[off[i] + q].u)
+                    return fail(NICE_ERR_HIP, "self-check: unique count of a listed number does not recompute");
         }
-        std::vector<uint32_t> u(n);
-        hipError_t err = hipMemcpyAsync(d.chk_n, pairs.data(), n * 16, hipMemcpyHostToDevice, d.aux);
-        if (err == hipSuccess) err = nice::launch_unique_counts(d.chk_n, (uint32_t)n, base, d.chk_u, d.aux);
-        if (err == hipSuccess) err = hipMemcpyAsync(u.data(), d.chk_u, n * 4, hipMemcpyDeviceToHost, d.aux);
-        if (err == hipSuccess) err = hipStreamSynchronize(d.aux);
-        if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("self-check: ") + hipGetErrorString(err));
-        for (size_t i = 0; i < n; i++)
-            if (u[i] != job.all[i].u)
-                return fail(NICE_ERR_HIP, "self-check: unique count of a listed number does not recompute");
     }
     std::sort(job.all.begin(), job.all.end(), [](const Entry &a, const Entry &b) { return a.n < b.n; });
     return NICE_OK;
@@ -884,36 +939,66 @@ int nice_last_kernel_stats(nice_ctx *ctx, int i, nice_kernel_stats *out) {
     return NICE_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+int detailed_submit_args(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, uint64_t end_lo, uint64_t end_hi,
+                         uint32_t base, bool wait, int *ticket) {
+    if (!ctx || !ticket) return fail(NICE_ERR_INVALID, "null argument");
+    if (base < 2 || base > 128) return fail(NICE_ERR_INVALID, "base must be in 2..=128");
+    const u128 s = mk(start_lo, start_hi), e = mk(end_lo, end_hi);
+    if (s >= e)
+        return fail(NICE_ERR_INVALID, "Range has invalid bounds, range_start must be < range_end");
+    std::unique_lock<std::mutex> lock(ctx->mu);
+    return detailed_submit(ctx, lock, s, e, base, wait, ticket);
+}
+
+int detailed_collect_locked(nice_ctx *ctx, int ticket, uint64_t *hist, nice_number *out, size_t cap,
+                            size_t *n_out);
+
+}  // namespace
+
+extern "C" {
+
 int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi,
                                 uint64_t end_lo, uint64_t end_hi, uint32_t base, uint64_t *hist,
                                 nice_number *out, size_t cap, size_t *n_out) {
     int t = -1;
-    int rc = nice_detailed_submit(ctx, start_lo, start_hi, end_lo, end_hi, base, &t);
+    int rc = detailed_submit_args(ctx, start_lo, start_hi, end_lo, end_hi, base, true, &t);
     if (rc) return rc;
     rc = nice_detailed_collect(ctx, t, hist, out, cap, n_out);
     if (rc == NICE_ERR_CAPACITY) {
         // synchronous call: the caller retries the whole field with room
-        std::lock_guard<std::mutex> lock(ctx->mu);
-        ctx->det[t].active = false;
-        ctx->det[t].all = {};
+        {
+            std::lock_guard<std::mutex> lock(ctx->mu);
+            ctx->det[t].active = false;
+            ctx->det[t].all = {};
+        }
+        ctx->freed.notify_all();
     }
     return rc;
 }
 
 int nice_detailed_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, uint64_t end_lo,
                          uint64_t end_hi, uint32_t base, int *ticket) {
-    if (!ctx || !ticket) return fail(NICE_ERR_INVALID, "null argument");
-    if (base < 2 || base > 128) return fail(NICE_ERR_INVALID, "base must be in 2..=128");
-    const u128 s = mk(start_lo, start_hi), e = mk(end_lo, end_hi);
-    if (s >= e)
-        return fail(NICE_ERR_INVALID, "Range has invalid bounds, range_start must be < range_end");
-    std::lock_guard<std::mutex> lock(ctx->mu);
-    return detailed_submit(ctx, s, e, base, ticket);
+    return detailed_submit_args(ctx, start_lo, start_hi, end_lo, end_hi, base, false, ticket);
 }
 
 int nice_detailed_collect(nice_ctx *ctx, int ticket, uint64_t *hist, nice_number *out, size_t cap,
                           size_t *n_out) {
     if (!ctx || !hist) return fail(NICE_ERR_INVALID, "null argument");
+    const int rc = detailed_collect_locked(ctx, ticket, hist, out, cap, n_out);
+    ctx->freed.notify_all();  // the ticket's slot may be free now
+    return rc;
+}
+
+}  // extern "C"
+
+namespace {
+
+int detailed_collect_locked(nice_ctx *ctx, int ticket, uint64_t *hist, nice_number *out, size_t cap,
+                            size_t *n_out) {
     std::unique_lock<std::mutex> lock(ctx->mu);
     if (ticket < 0 || ticket >= kSlots || !ctx->det[ticket].active)
         return fail(NICE_ERR_INVALID, "no detailed field in flight under this ticket");
@@ -942,6 +1027,10 @@ int nice_detailed_collect(nice_ctx *ctx, int ticket, uint64_t *hist, nice_number
     }
     return detailed_collect(ctx, ticket, hist, out, cap, n_out);
 }
+
+}  // namespace
+
+extern "C" {
 
 int nice_validate_detailed(uint32_t base, uint64_t size_lo, uint64_t size_hi, const uint64_t *hist,
                            const nice_number *list, size_t n) {
@@ -1197,6 +1286,8 @@ double nice_adaptive_floor_step(double floor, double msd_seconds, double total_s
     return std::min(kFloorMax, std::max(kFloorMin, floor * factor));
 }
 
+uint32_t nice_host_threads(void) { return available_parallelism(); }
+
 int nice_adaptive_floor(double *floor, uint32_t *warmup) {
     std::lock_guard<std::mutex> g(g_af_mu);
     const AdaptiveFloor &af = adaptive_floor();
@@ -1237,7 +1328,9 @@ int niceonly_enqueue(nice_ctx *ctx, int t, NiceJob &job) {
     const uint64_t floor_size = job.st.msd_floor;
     st.msd_floor = floor_size;
     const uint32_t k = opts && opts->stride_k ? opts->stride_k : 2;
-    int threads = opts && opts->threads > 0 ? opts->threads : (int)std::thread::hardware_concurrency();
+    // the reference sizes its MSD producer pool with available_parallelism()
+    // (client_process_gpu.rs:598): on a 16-CPU cgroup of a 256-CPU host, 16
+    int threads = opts && opts->threads > 0 ? opts->threads : (int)available_parallelism();
     if (threads < 1) threads = 1;
     const u128 chunk = opts && opts->chunk_size ? (u128)opts->chunk_size : nice::client_chunk_size(e - s);
     const uint64_t deal_stride = opts && opts->deal_stride ? opts->deal_stride : 1;
@@ -1493,6 +1586,7 @@ int niceonly_enqueue(nice_ctx *ctx, int t, NiceJob &job) {
         std::condition_variable qcv;
         std::deque<std::vector<std::pair<u128, u128>>> queue;
         const int n_workers = (int)std::min<uint64_t>(threads, mine);
+        st.msd_threads = (uint32_t)n_workers;
         int live = n_workers;  // guarded by qmu
         std::vector<std::thread> workers;
         std::unique_ptr<nice::MsdRunner> filt = nice::make_msd(base);
@@ -1611,11 +1705,12 @@ int niceonly_enqueue(nice_ctx *ctx, int t, NiceJob &job) {
 }
 
 // Read a finished niceonly field's results from the devices (its events have
-// completed).  *grow receives, per device, the list length when it exceeded
-// that device's list capacity (0 otherwise).
-int niceonly_gather(nice_ctx *ctx, NiceJob &job, int t, std::vector<uint32_t> &grow) {
-    grow.assign(ctx->devs.size(), 0);
+// completed).  counts receives every device's list length; *over is set when
+// one exceeded its device's list capacity (that device's list was not read).
+int niceonly_gather(nice_ctx *ctx, NiceJob &job, int t, std::vector<uint32_t> &counts, bool *over_out) {
+    counts.assign(ctx->devs.size(), 0);
     bool over = false;
+    *over_out = false;
     for (size_t i = 0; i < ctx->devs.size(); i++) {
         Device &d = ctx->devs[i];
         Slot &sl = d.slot[t];
@@ -1644,11 +1739,12 @@ int niceonly_gather(nice_ctx *ctx, NiceJob &job, int t, std::vector<uint32_t> &g
             job.st.square_ok += c[27];
         }
         const uint32_t cnt = *sl.h_nice;
+        counts[i] = cnt;
         if (cnt > sl.nice.cap) {
             // more nice numbers than the device list holds (the kernels count
             // every hit, store those below the capacity): grow and re-run
-            grow[i] = cnt;
             over = true;
+            *over_out = true;
             continue;
         }
         if (cnt && !over) {
@@ -1664,8 +1760,12 @@ int niceonly_gather(nice_ctx *ctx, NiceJob &job, int t, std::vector<uint32_t> &g
 
 extern "C" {
 
-int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, uint64_t end_lo,
-                         uint64_t end_hi, uint32_t base, const nice_niceonly_opts *opts, int *ticket) {
+}  // extern "C"
+
+namespace {
+
+int niceonly_submit_args(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, uint64_t end_lo, uint64_t end_hi,
+                         uint32_t base, const nice_niceonly_opts *opts, bool wait, int *ticket) {
     const auto t0 = std::chrono::steady_clock::now();
     if (!ctx || !ticket) return fail(NICE_ERR_INVALID, "null argument");
     if (base < 3 || base > 128) return fail(NICE_ERR_INVALID, "base must be in 3..=128");
@@ -1675,12 +1775,12 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
     if (opts && opts->deal_offset >= (opts->deal_stride ? opts->deal_stride : 1u))
         return fail(NICE_ERR_INVALID, "deal_offset must be < deal_stride");
     const uint64_t floor_size = resolve_floor(opts);
-    std::lock_guard<std::mutex> lock(ctx->mu);
-    const int t = free_slot(ctx->nice, ctx->nice_next);
-    if (t < 0)
-        return fail(NICE_ERR_INVALID, "three niceonly fields already in flight on this context; collect one first");
+    std::unique_lock<std::mutex> lock(ctx->mu);
+    int t = -1;
+    if (int rc = acquire_slot(ctx, lock, ctx->nice, ctx->nice_next, wait, "niceonly", &t)) return rc;
     NiceJob &job = ctx->nice[t];
     job = NiceJob{};
+    job.owner = std::this_thread::get_id();
     job.s = s;
     job.e = e;
     job.base = base;
@@ -1696,9 +1796,8 @@ int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, ui
     return NICE_OK;
 }
 
-int nice_niceonly_collect(nice_ctx *ctx, int t, nice_number *out, size_t cap, size_t *n_out,
-                          nice_niceonly_stats *stats) {
-    if (!ctx) return fail(NICE_ERR_INVALID, "null ctx");
+int niceonly_collect_locked(nice_ctx *ctx, int t, nice_number *out, size_t cap, size_t *n_out,
+                            nice_niceonly_stats *stats) {
     std::unique_lock<std::mutex> lock(ctx->mu);
     if (t < 0 || t >= kSlots || !ctx->nice[t].active)
         return fail(NICE_ERR_INVALID, "no niceonly field in flight under this ticket");
@@ -1722,23 +1821,32 @@ int nice_niceonly_collect(nice_ctx *ctx, int t, nice_number *out, size_t cap, si
             lock.lock();
             job.waiting = false;
         }
-        std::vector<uint32_t> grow;
-        if (!rc && !job.empty) rc = niceonly_gather(ctx, job, t, grow);
-        for (uint32_t attempt = 0; !rc && !job.empty; attempt++) {
-            bool over = false;
-            for (uint32_t g : grow) over |= g != 0;
-            if (!over) break;
+        std::vector<uint32_t> counts;
+        bool over = false;
+        if (!rc && !job.empty) rc = niceonly_gather(ctx, job, t, counts, &over);
+        for (uint32_t attempt = 0; !rc && !job.empty && over; attempt++) {
             if (attempt) {
                 rc = fail(NICE_ERR_HIP, "niceonly list overflowed again after growing it to the field's count");
                 break;
             }
-            // Grow the overflowing devices' lists to the counts the kernels
-            // reported and re-run the field (under the lock: rare).
+            // Grow EVERY used device's list to the whole field's count and
+            // re-run the field (under the lock: rare).  The host MSD producer
+            // hands batches to devices in the order its threads finish chunks,
+            // so a re-run can put the hits on another device than the first
+            // run did; no device can hold more than the field's total.
+            uint64_t total = 0;
+            for (uint32_t c : counts) total += c;
+            if (total > 0xfffff000ull) {
+                rc = fail(NICE_ERR_HIP, "niceonly list longer than 2^32 entries");
+                break;
+            }
             for (size_t i = 0; i < ctx->devs.size() && !rc; i++)
-                if (grow[i]) rc = ensure_listbuf(ctx->devs[i], ctx->devs[i].slot[t].nice, (grow[i] + 4095u) & ~4095u, false);
+                if (job.used[i])
+                    rc = ensure_listbuf(ctx->devs[i], ctx->devs[i].slot[t].nice, ((uint32_t)total + 4095u) & ~4095u,
+                                        false);
             if (!rc) rc = niceonly_enqueue(ctx, t, job);
             if (!rc) job.reruns++;
-            if (!rc) rc = niceonly_gather(ctx, job, t, grow);
+            if (!rc) rc = niceonly_gather(ctx, job, t, counts, &over);
         }
         if (rc) {
             job.active = false;
@@ -1746,8 +1854,11 @@ int nice_niceonly_collect(nice_ctx *ctx, int t, nice_number *out, size_t cap, si
         }
         job.st.total_seconds =
             std::chrono::duration<double>(std::chrono::steady_clock::now() - job.t0).count();
+        job.st.reruns = job.reruns;
         job.collected = true;
-        if (job.adapt) {  // update_msd_floor (client_process_gpu.rs:551, 563-568, 130-157)
+        // A re-run field's MSD time covers its last run only while its total
+        // spans every run: the two do not balance, so it does not move the floor.
+        if (job.adapt && job.reruns == 0) {  // update_msd_floor (client_process_gpu.rs:551, 563-568, 130-157)
             // The GPU tail ends when the field's last device work does (its
             // end event), not when the caller gets round to collecting: the
             // reference times both phases inside one call (:541-551).
@@ -1779,18 +1890,38 @@ int nice_niceonly_collect(nice_ctx *ctx, int t, nice_number *out, size_t cap, si
     return rc;
 }
 
+}  // namespace
+
+extern "C" {
+
+int nice_niceonly_submit(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi, uint64_t end_lo,
+                         uint64_t end_hi, uint32_t base, const nice_niceonly_opts *opts, int *ticket) {
+    return niceonly_submit_args(ctx, start_lo, start_hi, end_lo, end_hi, base, opts, false, ticket);
+}
+
+int nice_niceonly_collect(nice_ctx *ctx, int t, nice_number *out, size_t cap, size_t *n_out,
+                          nice_niceonly_stats *stats) {
+    if (!ctx) return fail(NICE_ERR_INVALID, "null ctx");
+    const int rc = niceonly_collect_locked(ctx, t, out, cap, n_out, stats);
+    ctx->freed.notify_all();  // the ticket's slot may be free now
+    return rc;
+}
+
 int nice_process_range_niceonly_ex(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi,
                                    uint64_t end_lo, uint64_t end_hi, uint32_t base,
                                    const nice_niceonly_opts *opts, nice_number *out, size_t cap,
                                    size_t *n_out, nice_niceonly_stats *stats) {
     int t = -1;
-    int rc = nice_niceonly_submit(ctx, start_lo, start_hi, end_lo, end_hi, base, opts, &t);
+    int rc = niceonly_submit_args(ctx, start_lo, start_hi, end_lo, end_hi, base, opts, true, &t);
     if (rc) return rc;
     rc = nice_niceonly_collect(ctx, t, out, cap, n_out, stats);
     if (rc == NICE_ERR_CAPACITY) {
-        std::lock_guard<std::mutex> lock(ctx->mu);
-        ctx->nice[t].active = false;
-        ctx->nice[t].all = {};
+        {
+            std::lock_guard<std::mutex> lock(ctx->mu);
+            ctx->nice[t].active = false;
+            ctx->nice[t].all = {};
+        }
+        ctx->freed.notify_all();
     }
     return rc;
 }

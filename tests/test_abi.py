@@ -414,3 +414,34 @@ def test_c_host_example_cpu_mode(golden):
     if _lib.lib().nice_device_count(ctypes.byref(n)) != 0 or n.value == 0:
         rc, dist, nice, err = run_c_example("--gpu", "detailed", 10, "range")
         assert rc == 4 and not dist and "device" in err
+
+
+def test_host_threads_follow_the_affinity_mask():
+    """nice_host_threads (the host MSD pool's size at threads = 0) is
+    std::thread::available_parallelism(): under `taskset -c 0-1` it is 2
+    (client_process_gpu.rs:598), whatever the host's core count."""
+    import shutil
+    import subprocess
+    import sys
+    if not shutil.which("taskset"):
+        pytest.skip("taskset not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = "import nice_amd; print(nice_amd.api.host_threads())"
+    out = subprocess.run(["taskset", "-c", "0-1", sys.executable, "-c", code], cwd=root,
+                         capture_output=True, text=True, check=True).stdout
+    assert int(out.strip()) == 2
+    out = subprocess.run(["taskset", "-c", "0", sys.executable, "-c", code], cwd=root,
+                         capture_output=True, text=True, check=True).stdout
+    assert int(out.strip()) == 1
+
+
+def test_bad_submit_arguments_fail_at_once():
+    """A submit with a bad argument answers NICE_ERR_INVALID immediately (no
+    context needed to see it); NICE_ERR_BUSY is its own status."""
+    L = _lib.lib()
+    t = ctypes.c_int()
+    assert L.nice_detailed_submit(None, 5, 0, 10, 0, 40, ctypes.byref(t)) == _lib.NICE_ERR_INVALID
+    assert L.nice_niceonly_submit(None, 5, 0, 10, 0, 40, None, ctypes.byref(t)) == _lib.NICE_ERR_INVALID
+    assert _lib.NICE_ERR_BUSY not in (_lib.NICE_OK, _lib.NICE_ERR_INVALID, _lib.NICE_ERR_HIP,
+                                      _lib.NICE_ERR_CAPACITY, _lib.NICE_ERR_NO_DEVICE,
+                                      _lib.NICE_ERR_MSD_OVERFLOW)

@@ -1066,18 +1066,19 @@ def test_threads_share_a_context():
                     if (i + w + rep) % 4:
                         continue
                     t, tn = ct.c_int(), ct.c_int()
-                    # three fields per mode in flight per context: a busy
-                    # context answers NICE_ERR_INVALID, retried
+                    # three fields per mode in flight per context: a full
+                    # context answers NICE_ERR_BUSY (only that is retried: a
+                    # bad argument would fail at once)
                     for _ in range(100000):
                         rc = lib.nice_detailed_submit(c._h, *N.api._split(a), *N.api._split(b), base, t)
-                        if rc != N._lib.NICE_ERR_INVALID:
+                        if rc != N._lib.NICE_ERR_BUSY:
                             break
                         time.sleep(0.0002)
                     assert rc == 0, lib.nice_last_error()
                     for _ in range(100000):
                         rn = lib.nice_niceonly_submit(c._h, *N.api._split(a), *N.api._split(b), base,
                                                       N.GpuContext._nice_opts(), tn)
-                        if rn != N._lib.NICE_ERR_INVALID:
+                        if rn != N._lib.NICE_ERR_BUSY:
                             break
                         time.sleep(0.0002)
                     assert rn == 0, lib.nice_last_error()
@@ -1106,3 +1107,153 @@ def test_threads_share_a_context():
         for det, nice in results:
             assert det == want_det[i], jobs[i]
             assert nice == want_nice[i], jobs[i]
+
+
+# --- round 5: shared-context blocking, BUSY, host MSD pool, 8 shards ---------
+def _raw_detailed(lib, ct, h, a, b, base, cap=1 << 14):
+    hist = (ct.c_uint64 * (base + 1))()
+    out = (N._lib.nice_number * cap)()
+    n = ct.c_size_t()
+    rc = lib.nice_process_range_detailed(h, *N.api._split(a), *N.api._split(b), base, hist, out, cap, n)
+    return rc, (list(hist), [(out[q].number_lo | (out[q].number_hi << 64), out[q].num_uniques)
+                             for q in range(min(n.value, cap))])
+
+
+def test_synchronous_calls_wait_for_a_slot():
+    """Eight host threads call the SYNCHRONOUS entry points on one context
+    with no retry loop (the reference shares one GpuContext across the
+    client's tasks and blocks behind its Mutex, client/src/main.rs:622,
+    client_process_gpu.rs:199-200): with three slots per mode, five threads
+    at a time find every slot in flight and must wait for another thread's
+    collect, never fail; every result equals the single-threaded one."""
+    import threading
+    lib = N._lib.lib()
+    ct = N._lib.ctypes
+    c = N.GpuContext(0)
+    s40, s80 = O.base_range(40)[0], O.base_range(80)[0]
+    jobs = [(s40 + k * 10 ** 7, s40 + k * 10 ** 7 + 2 * 10 ** 6, 40) for k in range(5)] + \
+           [(s80 + k * 10 ** 6, s80 + k * 10 ** 6 + 3 * 10 ** 5, 80) for k in range(3)]
+    want = [c.detailed_raw(a, b, base) for a, b, base in jobs]
+    want_nice = [c.niceonly_raw(a, b, base)[0] for a, b, base in jobs]
+    errors, got = [], []
+
+    def worker(w):
+        try:
+            for rep in range(4):
+                i = (w + rep) % len(jobs)
+                a, b, base = jobs[i]
+                rc, res = _raw_detailed(lib, ct, c._h, a, b, base)
+                assert rc == 0, (rc, lib.nice_last_error())
+                cap = 64
+                out = (N._lib.nice_number * cap)()
+                n = ct.c_size_t()
+                rn = lib.nice_process_range_niceonly_ex(c._h, *N.api._split(a), *N.api._split(b), base, None,
+                                                        out, cap, n, None)
+                assert rn == 0, (rn, lib.nice_last_error())
+                got.append((i, res, [out[q].number_lo | (out[q].number_hi << 64) for q in range(n.value)]))
+        except BaseException as e:
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(w,)) for w in range(8)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    c.close()
+    assert not errors, errors[0]
+    assert len(got) == 32
+    for i, res, nice in got:
+        assert res == want[i], jobs[i]
+        assert nice == want_nice[i], jobs[i]
+
+
+def test_busy_and_invalid_statuses():
+    """A full context answers NICE_ERR_BUSY to a submit (and to a synchronous
+    call from the thread that holds every slot, which no other thread could
+    free); a bad argument answers NICE_ERR_INVALID at once, busy or not."""
+    lib = N._lib.lib()
+    ct = N._lib.ctypes
+    c = N.GpuContext(0)
+    s = O.base_range(40)[0]
+    try:
+        tick = [c.detailed_submit(s + k * 10 ** 6, s + (k + 1) * 10 ** 6, 40) for k in range(3)]
+        t = ct.c_int()
+        assert lib.nice_detailed_submit(c._h, *N.api._split(s), *N.api._split(s + 10), 40, t) == N._lib.NICE_ERR_BUSY
+        rc, _ = _raw_detailed(lib, ct, c._h, s, s + 10, 40)
+        assert rc == N._lib.NICE_ERR_BUSY
+        assert lib.nice_detailed_submit(c._h, *N.api._split(s + 10), *N.api._split(s), 40, t) == N._lib.NICE_ERR_INVALID
+        assert lib.nice_detailed_submit(c._h, *N.api._split(s), *N.api._split(s + 10), 1, t) == N._lib.NICE_ERR_INVALID
+        ntick = [c.niceonly_submit(s + k * 10 ** 6, s + (k + 1) * 10 ** 6, 40) for k in range(3)]
+        assert lib.nice_niceonly_submit(c._h, *N.api._split(s), *N.api._split(s + 10), 40, None, t) == \
+            N._lib.NICE_ERR_BUSY
+        assert lib.nice_niceonly_submit(c._h, *N.api._split(s), *N.api._split(s + 10), 2, None, t) == \
+            N._lib.NICE_ERR_INVALID
+        got = [c.detailed_collect(x, 40) for x in tick]
+        assert got == [c.detailed_raw(s + k * 10 ** 6, s + (k + 1) * 10 ** 6, 40) for k in range(3)]
+        for x in ntick:
+            c.niceonly_collect(x)
+        # free again: the synchronous call goes through
+        rc, res = _raw_detailed(lib, ct, c._h, s, s + 10, 40)
+        assert rc == 0 and sum(res[0]) == 10
+    finally:
+        c.close()
+
+
+def test_host_msd_pool_is_available_parallelism(ctx):
+    """threads = 0 sizes the host MSD pool with available_parallelism() (the
+    affinity mask capped by the cgroup quota), as client_process_gpu.rs:598
+    does -- not hardware_concurrency (256 on the box's 16-CPU cgroup)."""
+    s = O.base_range(40)[0]
+    want = N.api.host_threads()
+    assert 1 <= want <= (os.cpu_count() or want)
+    lst, st = ctx.niceonly_raw(s, s + 10 ** 8, 40, msd_where="host")
+    assert st.msd_threads == min(want, 100)  # 100 chunks of 1e6
+    lst, st = ctx.niceonly_raw(s, s + 10 ** 8, 40, msd_where="host", threads=3)
+    assert st.msd_threads == 3
+    lst, st = ctx.niceonly_raw(s, s + 10 ** 8, 40, msd_where="device")
+    assert st.msd_threads == 0
+
+
+def test_eight_shard_context():
+    """The C-ABI multi-device context at a node's width: nice_ctx_create with
+    eight devices (all device 0 here: 8 shards, 24 slots of streams), as a
+    Rust client passing --gpu-device for all eight GPUs would create it
+    (client/src/main.rs:109-111; north_star's 8-way contiguous split).  The
+    whole extra-large field against the oracle fixture; an out-of-range b10
+    field whose every shard lists thousands of near-misses (merged across 8
+    lists, each shard's list self-checked on its own device); a massive
+    window with candidates on both MSD placements (the host producer deals
+    its batches over the 8 devices); and a 3-field submit/collect pipeline
+    collected out of order."""
+    c = N.GpuContext([0] * 8)
+    try:
+        f = _oracle_fields()
+        x = {d["name"]: d for d in f["detailed"]}["b40_extra_large_1e9"]
+        hist, lst = c.detailed_raw(int(x["start"]), int(x["end"]), 40)
+        assert _dist(hist) == [tuple(v) for v in x["distribution"]]
+        assert lst == [(int(n), u) for n, u in x["near_misses"]]
+        for y in f["niceonly"]:
+            nice, st = c.niceonly_raw(int(y["start"]), int(y["end"]), y["base"])
+            assert st.candidates == y["candidates"] and [str(n) for n in nice] == y["nice_numbers"], y["name"]
+        want = O.process_range_detailed(10 ** 6, 12 * 10 ** 5, 10, cap=2 * 10 ** 5)
+        hist, lst = c.detailed_raw(10 ** 6, 12 * 10 ** 5, 10)
+        assert _dist(hist) == want.distribution and lst == want.nice_numbers
+        assert len(lst) > 8 * 1000
+        m = _massive()
+        w = {int(v["start"]) - int(m["start"]): v for v in m["windows"]}[85 * 10 ** 11]
+        for where in ("device", "host"):
+            nice, st = c.niceonly_raw(int(w["start"]), int(w["end"]), 50, chunk_size=m["chunk"], msd_where=where)
+            assert (st.candidates, st.ranges) == (w["candidates"], w["ranges"]), where
+            assert [str(n) for n in nice] == w["nice_numbers"]
+        s = O.base_range(40)[0]
+        fields = [(s + k * 10 ** 8, s + k * 10 ** 8 + 3 * 10 ** 7 + k, 40) for k in range(3)]
+        td = [c.detailed_submit(a, b, base) for a, b, base in fields]
+        tn = [c.niceonly_submit(a, b, base) for a, b, base in fields]
+        got_d = {k: c.detailed_collect(td[k], 40) for k in (2, 0, 1)}
+        got_n = {k: c.niceonly_collect(tn[k])[0] for k in (1, 2, 0)}
+        for k, (a, b, base) in enumerate(fields):
+            assert got_d[k] == ctx_timed_detailed(a, b, base)
+            want_n, cands = O.process_field_niceonly_mt(a, b, base, 4)
+            assert got_n[k] == [n for n, _ in want_n.nice_numbers]
+    finally:
+        c.close()
