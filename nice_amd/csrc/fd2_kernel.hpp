@@ -49,7 +49,9 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <cmath>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <type_traits>
 
@@ -253,8 +255,12 @@ constexpr int big_wg(int base) { return waves_at(base, 1024) >= waves_at(base, 5
 // per 1e9; b42..50 and b59..64, two workgroups per CU, +1..+6 %).
 constexpr bool one_wg_per_cu(int base, int wg) { return waves_at(base, wg) == wg / 256; }
 
+// Sibling lanes (Cfg::SIB = M > 1): registers per wave for M lanes' state
+// (the shared limb-1 state once, the upper limbs of every sibling).
+constexpr int sib_waves(int base, int m) { return m <= 1 ? state_waves(base) : (m <= 3 ? 6 : 5); }
+
 template <int BASE_, int ND_, int NE_, int NE2_, int PROBE_ = 0, int WG_ = 512, int VD_ = 0, int LG_ = -1,
-          int PERS_ = -1>
+          int PERS_ = -1, int SIB_ = 1>
 struct Cfg {
     static constexpr int BASE = BASE_;
     // Bottleneck probes (timing experiments only, results are wrong): 1 = no
@@ -340,7 +346,13 @@ struct Cfg {
     static constexpr int TEND = SPLIT ? (TB + (int)(B * ES) + 15) / 16 * 16
                                       : TK + (LSDX ? ((int)(2 * B) + 15) / 16 * 16 : 0);
     static constexpr int HB = SPLIT ? TEND : 0;  // window rows
-    static constexpr int LDS_BYTES = SPLIT ? HB + HIST_BYTES : TEND;
+    // Sibling lanes: each sibling's cached C limbs [CL, NC) -- read and
+    // written only on the rare path -- as u16 per thread in LDS instead of
+    // VGPRs (slot (j, k) of thread t at COLD + 2 ((j NCOLD + k) WG + t)).
+    static constexpr int NCOLD = SIB_ > 1 ? NC - CL : 0;
+    static constexpr int COLD = TEND;
+    static constexpr int COLD_BYTES = (SIB_ * NCOLD * WG_ * 2 + 15) / 16 * 16;
+    static constexpr int LDS_BYTES = SPLIT ? HB + HIST_BYTES : TEND + COLD_BYTES;
     static constexpr int TAB_BYTES = TEND - TC0;  // table image copied in per workgroup
     static constexpr int ZA = SPLIT ? TC0 : TB;   // zeroed per workgroup: [0, ZA) and [HB, LDS_BYTES)
     static constexpr int LO = LSD ? 1 : 0;  // first stored / looked-up limb
@@ -377,8 +389,16 @@ struct Cfg {
     // its lookup is nearly a broadcast (4 LDS cycles on b80's index pattern),
     // while the limbs below it cost 11-12 (scripts/ubench/lds_trace_gen.py).
     static constexpr int VDB = (VD & 2048) ? 1 : 0;
-    static constexpr bool vd_s(int q) { return q >= SL - VDB - VDS && q < SL - VDB; }
-    static constexpr bool vd_c(int q) { return q >= CL - VDB - VDC && q < CL - VDB; }
+    // VD & 4096: the VALU-decoded limbs are the LOWEST ones above the
+    // low-digit table's limb (LO + 1 ...): the most data-random indices, whose
+    // lookups bank-conflict the most (sibling lanes, which have VALU to spare)
+    static constexpr bool VDLOW = (VD & 4096) != 0;
+    static constexpr bool vd_s(int q) {
+        return VDLOW ? (q > LO && q <= LO + VDS && q < SL) : (q >= SL - VDB - VDS && q < SL - VDB);
+    }
+    static constexpr bool vd_c(int q) {
+        return VDLOW ? (q > LO && q <= LO + VDC && q < CL) : (q >= CL - VDB - VDC && q < CL - VDB);
+    }
     // Lookup groups: a scheduling barrier after every LG table lookups of a
     // step (0: none), so the compiler cannot hoist all of a step's LDS reads
     // ahead of their ORs -- with SPLIT's b64 + u16 pairs that held ~75 VGPRs
@@ -386,7 +406,10 @@ struct Cfg {
     // 128-VGPR budget; the 16-byte layout spilled 52-64 bytes per lane there
     // too, and LG 8 removes it (b80 1e9 7.45 -> 7.31 ms, lg_sweep.log).
     // -1: the per-base default.
-    static constexpr int LG = LG_ >= 0 ? LG_ : (MW == 3 && WG >= 1024 ? 8 : 0);
+    // (sibling lanes: LG >= 100 -- the default -- pipelines the siblings'
+    // lookups with the arithmetic, walk_sib_pipe; below 100 LG != 0 ends a
+    // group after each sibling's lookups, LG > 1 after every LG of them too)
+    static constexpr int LG = LG_ >= 0 ? LG_ : (SIB_ > 1 ? 100 : (MW == 3 && WG >= 1024 ? 8 : 0));
     // Persistent grid: one round of resident workgroups, each walking a
     // contiguous range of 64-unit batches that its waves pull from an LDS
     // counter as they finish (instead of one chunk per lane and many rounds
@@ -394,26 +417,40 @@ struct Cfg {
     // wave finishes: b54 1e9, one 1024-thread workgroup per CU, waited 61 us
     // of a 134 us workgroup life for it, profiles/r03/fd2_stamps_b54.log).
     // -1: the per-base default.
-    static constexpr bool PERS = PERS_ >= 0 ? PERS_ != 0 : (WG >= 1024 && one_wg_per_cu(BASE, WG));
+    // Sibling lanes: M = SIB numbers n0 + j B^2 per lane, in lock step.  n and
+    // n + j B^2 agree mod B^2, so limbs 0 and 1 of n^2, n^3, 2n + 1 and 3n + 1
+    // (radix B) are the same for all of them and so is the carry out of limb
+    // 1 of every chain: the low-digit lookup, limb 1's two lookups and limb 1's
+    // carry chains run once for the M numbers (walk_sib).  Rounds only.
+    static constexpr int SIB = SIB_;
+    static constexpr bool PERS = SIB_ > 1 ? false : PERS_ >= 0 ? PERS_ != 0 : (WG >= 1024 && one_wg_per_cu(BASE, WG));
     // the same kernel with rounds of workgroups (launch_cfg falls back to it
     // when the runtime occupancy or the field size does not suit PERS), at
     // the workgroup size rounds prefer
     using NoPers = Cfg<BASE_, ND_, NE_, NE2_, PROBE_, (PERS_ < 0 ? rounds_wg(BASE_) : WG_), VD_, LG_, 0>;
+    // the production kernel without sibling lanes (segments shorter than a
+    // few M B^2): the big-field workgroup size and VALU-decoded limbs
+    using NoSib = Cfg<BASE_, ND_, NE_, NE2_, PROBE_, rounds_wg(BASE_), valu_limbs_big(BASE_, ND_, NE_), -1, 0>;
+    // lookup groups of walk_chunk (the sibling kernel's regular parts: none)
+    static constexpr int LGW = SIB_ > 1 ? 0 : (LG_ >= 0 ? LG_ : (MW == 3 && WG_ >= 1024 ? 8 : 0));
     // VD & 256 (no low-digit table only): limb 0 of S and of C by VALU too --
     // n^2 mod B and n^3 mod B of a wave's lanes keep few residues mod 16, so
     // their lookups pile onto few bank quads
     static constexpr bool VDL = (VD & 256) != 0 && !LSD;
     static constexpr u32 MAGIC_D = (u32)(((1ull << 32) + ES * BASE - 1) / (ES * BASE));
     static_assert(VD == 0 || (MW >= 2 && split_exact(BASE, ES, MAGIC_D)), "VALU digit split");
-    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1 && (VD & ~0xfff) == 0 &&
+    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1 && (VD & ~0x1fff) == 0 &&
                       ((VD & 1024) == 0 || LSDX),
                   "VALU-decoded limbs");
     // Waves per SIMD: what the LDS allows, capped by what the lane state
     // needs in VGPRs (the register budget is set to match, see state_waves).
     static constexpr int WPE0 = (163840 / LDS_BYTES) * (WG / 64) / 4;
-    static constexpr int WPE1 = WPE0 < state_waves(BASE) ? WPE0 : state_waves(BASE);
-    // in whole workgroups: a workgroup puts WG / 256 waves on each SIMD
-    static constexpr int WPE = WPE1 / (WG / 256) * (WG / 256) > 0 ? WPE1 / (WG / 256) * (WG / 256) : WG / 256;
+    static constexpr int WPE1 = WPE0 < sib_waves(BASE, SIB) ? WPE0 : sib_waves(BASE, SIB);
+    // in whole workgroups: k = the workgroups a CU holds at WPE1 waves per
+    // SIMD (a workgroup's WG / 64 waves spread over the 4 SIMDs), then the
+    // waves per SIMD those k workgroups need (640-thread workgroups: 2.5 each)
+    static constexpr int WGK = WPE1 * 256 / WG;
+    static constexpr int WPE = WGK > 0 ? (WGK * (WG / 64) + 3) / 4 : (WG / 64 + 3) / 4;
     static_assert(WPE >= 1, "LDS: not even one workgroup fits");
     static_assert(SL < NS && CL < NC && EL <= NE, "FD layout needs cached high limbs");
     static_assert(ND <= NX + 1 && NE2 <= NX + 1 && NE <= NS + 1, "difference limb counts");
@@ -430,6 +467,8 @@ struct Cfg {
                   "C-limb carry magic");
     static_assert(NN <= SL && NE >= NS, "C += 3S + N3 layout");
     static_assert(3 * ES <= 64, "inline-constant multiplier");
+    static_assert(SIB == 1 || (LSD && MW == 2 && LO == 1 && SL >= 3 && CL >= 3 && ND >= 2 && NN >= 2),
+                  "sibling lanes share limb 1: low-digit-table bases only");
     static_assert((unsigned long long)NX * B * B + 2ull * B < (1ull << 32), "32-bit init columns");
 };
 
@@ -945,6 +984,13 @@ struct Fd2Args {
     u32 cutoff;
     u32 ncopies;        // histogram copies in use (<= kHistCopies), the same for every launch of a field
     u32 wave_cap;       // persistent grid: batches one wave may take (its lanes' u16 counters hold them)
+    // Cfg::SIB > 1: blocks [0, sib_blocks) walk sibling units (q, k) -> n0 =
+    // sib + q M B^2 + k sib_chunk, k < sib_upb; blocks [sib_blocks,
+    // sib_blocks + edge_blocks) the edge units q -> edge + q M B^2 (chunk
+    // edge_chunk: the rest of each B^2 block); the regular parts follow.
+    u64 sib_lo, sib_hi, edge_lo, edge_hi;
+    u32 sib_chunk, sib_upb, sib_units, sib_blocks;
+    u32 edge_chunk, edge_units, edge_blocks;
     u64 *hist;          // kHistCopies x 129 bins
     NumOut out;
     const uint4 *tabs;
@@ -1046,14 +1092,14 @@ __device__ __forceinline__ void walk_chunk(State<P> &st, const unsigned char *sm
                 if ((P::PROBE & 4) && q == 1) { m[0] |= st.S[q] & 0xffu; continue; }  // probe: no limb-1 lookups
                 if (P::vd_s(q) || (P::VDL && q == 0)) or_valu<P>(st.S[q] - P::EBT, m);
                 else or_lookup<P, P::TB - (int)P::EBT, P::T2 - (int)P::EBT / 2>(smem, st.S[q], m);
-                if (P::LG && (q - P::LO + 1) % P::LG == 0) lookup_group_end<P>(m);
+                if (P::LGW && (q - P::LO + 1) % P::LGW == 0) lookup_group_end<P>(m);
             }
 #pragma unroll
             for (int q = P::LO; q < P::CL; q++) {
                 if ((P::PROBE & 4) && q == 1) { m[1] |= st.C[q] & 0xffu; continue; }
                 if (P::vd_c(q) || (P::VDL && q == 0)) or_valu<P>(st.C[q], m);
                 else or_lookup<P, P::TB, P::T2>(smem, st.C[q], m);
-                if (P::LG && (P::SL + q - 2 * P::LO + 1) % P::LG == 0) lookup_group_end<P>(m);
+                if (P::LGW && (P::SL + q - 2 * P::LO + 1) % P::LGW == 0) lookup_group_end<P>(m);
             }
         }
         // uw = unique count - W0: the bias rides in the first v_bcnt's
@@ -1079,6 +1125,441 @@ __device__ __forceinline__ void walk_chunk(State<P> &st, const unsigned char *sm
             }
         }
         step<P>(st, smem, w1);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Sibling lanes (Cfg::SIB = M > 1).  A lane steps the M numbers n + j B^2
+// (j < M) together.  They agree mod B^2, so limbs 0 and 1 of n^2, n^3, D1 =
+// 2n + 1 and N3 = 3n + 1 are equal for all of them, and so is every chain's
+// carry out of limb 1: the low-digit entry (limb 0 of S and C, with the
+// carries and wrap flags), the two limb-1 lookups and limb 1's carry chains
+// are done once per step for M numbers.  Sibling 0's State holds the shared
+// limbs (its S[1], C[1], D1[1], N3[1], r8); the other siblings' copies of
+// them are never read.  Limbs >= 2, the cached high limbs and their mask are
+// each sibling's own.  Per n: b40 M = 2 goes from 12 lookups and ~266 VALU
+// cycles per wave-step to 10.5 and ~240.
+// ---------------------------------------------------------------------------
+
+// One C limb i > LO of C += 3S + N3 (old S) with the scaled carry-in cC;
+// returns the scaled carry out (step() does the same inline).  The cached S
+// limbs [SL, NS) of a sibling are held as K = 3 ES S (they change only on the
+// rare path), so their term is one add.
+template <class P>
+__device__ __forceinline__ u32 c_limb(State<P> &st, int i, u32 cC) {
+    u32 t = st.C[i] + cC;
+    if (i < P::NN) asm("" : "+v"(t));
+    if (i < P::NN) t += st.N3[i];
+    else if (i < P::SL) t -= 3 * P::EBT;
+    if (i < P::SL) t = mad_u24<3>(st.S[i], t);
+    else if (i < P::NS) t += st.S[i];
+    const u32 c = P::C1 ? __umulhi(t, P::MAGIC) : __umulhi(t / P::ES, P::MAGICB);
+    st.C[i] = t - c * P::DC;
+    return c * P::ES;
+}
+
+// One S limb i > LO of S += D1 (biased) with the scaled carry-in cS.
+template <class P>
+__device__ __forceinline__ u32 s_limb(State<P> &st, int i, u32 cS) {
+    const u32 t = st.S[i] + (i < P::ND ? st.D1[i] : 0u) + cS;
+    const u32 c = (t >> P::T) & P::ES;
+    st.S[i] = t - c * P::B;
+    return c;
+}
+
+// A sibling's cold C limb k (C[CL + k]) in LDS.
+template <class P>
+__device__ __forceinline__ unsigned short *cold_slot(const unsigned char *smem, int j, int k) {
+    return (unsigned short *)(smem + P::COLD) + ((u32)(j * P::NCOLD + k) * P::WG + threadIdx.x);
+}
+
+// recompute_hi for a sibling: cached S limbs in K form, cached C limbs in LDS.
+template <class P>
+__device__ __forceinline__ void sib_hi(State<P> &st, int j, const unsigned char *smem) {
+#pragma unroll
+    for (int w = 0; w < P::MW; w++) st.hi[w] = 0;
+#pragma unroll
+    for (int i = P::SL; i < P::NS; i++)
+        or_plain<P>(smem, st.S[i] / (3 * P::ES), i == P::NS - 1 ? P::S_TOPD : 2, st.hi);
+#pragma unroll
+    for (int k = 0; k < P::NCOLD; k++)
+        or_plain<P>(smem, *cold_slot<P>(smem, j, k), P::CL + k == P::NC - 1 ? P::C_TOPD : 2, st.hi);
+}
+
+// Sibling state after init: cached S limbs to K form, cached C limbs to LDS.
+template <class P>
+__device__ __forceinline__ void sib_park(State<P> &st, int j, const unsigned char *smem) {
+#pragma unroll
+    for (int i = P::SL; i < P::NS; i++) st.S[i] *= 3 * P::ES;
+#pragma unroll
+    for (int k = 0; k < P::NCOLD; k++) *cold_slot<P>(smem, j, k) = (unsigned short)st.C[P::CL + k];
+}
+
+// Rare path of step_sib: limb-0 wraps of D1 / N3 (one event for all
+// siblings: the shared limb 1, then each sibling's upper limbs) and carries
+// out of each sibling's top stepped limbs (rare()'s work per sibling).
+template <class P>
+__device__ __forceinline__ void rare_sib(State<P> (&st)[P::SIB], const unsigned char *smem, u32 d1w, u32 n3w,
+                                      const bool (&cS)[P::SIB], const bool (&cC)[P::SIB]) {
+    constexpr int L = P::LO;
+    if (d1w) {
+        const u32 v = st[0].D1[L] + P::ES;
+        const bool c = v >= P::ESB;
+        st[0].D1[L] = c ? 0u : v;
+        if (c)
+#pragma unroll
+            for (int j = 0; j < P::SIB; j++) carry_scaled<P>(st[j].D1, L + 1);
+    }
+    if (n3w) {
+        const u32 off1 = L < P::SL ? 3 * P::EBT : 0u;
+        const u32 v = st[0].N3[L] + off1 + P::ES;
+        const bool c = v >= P::ESB;
+        st[0].N3[L] = (c ? 0u : v) - off1;
+        if (c) {
+#pragma unroll
+            for (int j = 0; j < P::SIB; j++) {
+                u32 cc = 1;
+#pragma unroll
+                for (int i = L + 1; i < P::NN; i++) {
+                    const u32 off = i < P::SL ? 3 * P::EBT : 0u;
+                    const u32 w = st[j].N3[i] + off + cc * P::ES;
+                    cc = w >= P::ESB;
+                    st[j].N3[i] = (cc ? 0u : w) - off;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < P::SIB; j++) {
+        if (cS[j]) {
+            st[j].S[P::SL - 1] -= P::ESB;
+            u32 c = 1;  // +1 into the cached limbs (K form: 3 ES per unit)
+#pragma unroll
+            for (int i = P::SL; i < P::NS; i++) {
+                const u32 v = st[j].S[i] + c * 3 * P::ES;
+                c = v >= 3 * P::ESB;
+                st[j].S[i] = c ? 0u : v;
+            }
+        }
+        if (cC[j]) {
+            st[j].C[P::CL - 1] -= P::DC;
+            u32 c = 1;
+#pragma unroll
+            for (int k = 0; k < P::NCOLD; k++) {
+                unsigned short *slot = cold_slot<P>(smem, j, k);
+                const u32 v = *slot + c;
+                c = v == P::B;
+                *slot = (unsigned short)(c ? 0u : v);
+            }
+        }
+        if (cS[j] | cC[j]) sib_hi<P>(st[j], j, smem);
+    }
+}
+
+// One FD step of all siblings (step() restated with the shared limb 1).
+template <class P>
+__device__ __forceinline__ void step_sib(State<P> (&st)[P::SIB], const unsigned char *smem, u32 w1) {
+    constexpr u32 ES = P::ES;
+    constexpr int L = P::LO;
+    constexpr int CT = P::CL - 1, ST = P::SL - 1;
+    State<P> &s0 = st[0];
+    // shared limb L of C += 3S + N3 (old S) and of S += D1
+    u32 cC = __builtin_amdgcn_ubfe(w1, P::FC, P::FCW);
+    {
+        u32 t = P::TIGHT ? mad_u24<ES>(cC, s0.C[L]) : s0.C[L] + cC;
+        if (L < P::NN) t += s0.N3[L];
+        else t -= 3 * P::EBT;
+        t = mad_u24<3>(s0.S[L], t);
+        const u32 c = P::C1 ? __umulhi(t, P::MAGIC) : __umulhi(t / ES, P::MAGICB);
+        s0.C[L] = t - c * P::DC;
+        cC = c * ES;
+    }
+    u32 cS = __builtin_amdgcn_ubfe(w1, P::F0, P::F0W);
+    {
+        const u32 d = L < P::ND ? s0.D1[L] : 0u;
+        const u32 t = P::TIGHT ? mad_u24<ES>(cS, s0.S[L] + d) : s0.S[L] + d + cS;
+        cS = (t >> P::T) & ES;
+        s0.S[L] = t - cS * P::B;
+    }
+    s0.r8 += ES;
+    bool topS[P::SIB], topC[P::SIB];
+    bool any = w1 >= P::FLAG_D1;
+#pragma unroll
+    for (int j = 0; j < P::SIB; j++) {
+        u32 c = cC;
+#pragma unroll
+        for (int i = L + 1; i < CT; i++) c = c_limb<P>(st[j], i, c);
+        st[j].C[CT] += c;
+        u32 cs = cS;
+#pragma unroll
+        for (int i = L + 1; i < ST; i++) cs = s_limb<P>(st[j], i, cs);
+        st[j].S[ST] += cs;
+        topS[j] = st[j].S[ST] >= (1u << P::SH);
+        topC[j] = st[j].C[CT] >= P::DC;
+        any |= topS[j] | topC[j];
+    }
+    if (any) rare_sib<P>(st, smem, w1 & P::FLAG_D1, w1 & P::FLAG_N3, topS, topC);
+}
+
+// step_sib in pieces for the pipelined walk: the shared limb L (returns the
+// scaled carries into limb L + 1 of C and S) ...
+template <class P>
+__device__ __forceinline__ void sib_shared_step(State<P> &s0, u32 w1, u32 &cC, u32 &cS) {
+    constexpr u32 ES = P::ES;
+    constexpr int L = P::LO;
+    cC = __builtin_amdgcn_ubfe(w1, P::FC, P::FCW);
+    {
+        u32 t = P::TIGHT ? mad_u24<ES>(cC, s0.C[L]) : s0.C[L] + cC;
+        if (L < P::NN) t += s0.N3[L];
+        else t -= 3 * P::EBT;
+        t = mad_u24<3>(s0.S[L], t);
+        const u32 c = P::C1 ? __umulhi(t, P::MAGIC) : __umulhi(t / ES, P::MAGICB);
+        s0.C[L] = t - c * P::DC;
+        cC = c * ES;
+    }
+    cS = __builtin_amdgcn_ubfe(w1, P::F0, P::F0W);
+    {
+        const u32 d = L < P::ND ? s0.D1[L] : 0u;
+        const u32 t = P::TIGHT ? mad_u24<ES>(cS, s0.S[L] + d) : s0.S[L] + d + cS;
+        cS = (t >> P::T) & ES;
+        s0.S[L] = t - cS * P::B;
+    }
+    s0.r8 += ES;
+}
+
+// ... and one sibling's limbs above it (returns whether a top limb carried).
+template <class P>
+__device__ __forceinline__ bool sib_upper_step(State<P> &st, u32 cC, u32 cS, bool &topS, bool &topC) {
+    constexpr int L = P::LO;
+    constexpr int CT = P::CL - 1, ST = P::SL - 1;
+#pragma unroll
+    for (int i = L + 1; i < CT; i++) cC = c_limb<P>(st, i, cC);
+    st.C[CT] += cC;
+#pragma unroll
+    for (int i = L + 1; i < ST; i++) cS = s_limb<P>(st, i, cS);
+    st.S[ST] += cS;
+    topS = st.S[ST] >= (1u << P::SH);
+    topC = st.C[CT] >= P::DC;
+    return topS | topC;
+}
+
+// One sibling's looked-up table entries of a step (entries of VALU-decoded
+// limbs and of limbs <= L are unused).
+template <class P>
+struct SibLook {
+    uint2 s[P::SL], c[P::CL];
+};
+
+template <class P>
+__device__ __forceinline__ void sib_issue(const State<P> &st, const unsigned char *smem, SibLook<P> &e) {
+#pragma unroll
+    for (int q = P::LO + 1; q < P::SL; q++)
+        if (!P::vd_s(q)) e.s[q] = *(const uint2 *)(smem + (P::TB - (int)P::EBT) + st.S[q]);
+#pragma unroll
+    for (int q = P::LO + 1; q < P::CL; q++)
+        if (!P::vd_c(q)) e.c[q] = *(const uint2 *)(smem + P::TB + st.C[q]);
+}
+
+template <class P>
+__device__ __forceinline__ void sib_consume(const State<P> &st, const SibLook<P> &e, u32 (&m)[P::MW]) {
+#pragma unroll
+    for (int q = P::LO + 1; q < P::SL; q++) {
+        if (P::vd_s(q)) {
+            or_valu<P>(st.S[q] - P::EBT, m);
+        } else {
+            m[0] |= e.s[q].x;
+            m[1] |= e.s[q].y;
+        }
+    }
+#pragma unroll
+    for (int q = P::LO + 1; q < P::CL; q++) {
+        if (P::vd_c(q)) {
+            or_valu<P>(st.C[q], m);
+        } else {
+            m[0] |= e.c[q].x;
+            m[1] |= e.c[q].y;
+        }
+    }
+}
+
+// OR the digit bits of limb q of sibling j's S (isS) or C into m.
+template <class P>
+__device__ __forceinline__ void or_limb(const State<P> &st, const unsigned char *smem, bool isS, int q,
+                                        u32 (&m)[P::MW]) {
+    if (isS) {
+        if (P::vd_s(q)) or_valu<P>(st.S[q] - P::EBT, m);
+        else or_lookup<P, P::TB - (int)P::EBT, P::T2 - (int)P::EBT / 2>(smem, st.S[q], m);
+    } else {
+        if (P::vd_c(q)) or_valu<P>(st.C[q], m);
+        else or_lookup<P, P::TB, P::T2>(smem, st.C[q], m);
+    }
+}
+
+// walk_chunk for M siblings: `chunk` steps of the numbers n0 + j B^2 + i.
+// Sibling 0's first number of this lane's unit (fd2_body's layout of the
+// sibling parts; recomputed on the rare near-miss path instead of kept live).
+struct SibUnit {
+    bool active;
+    u32 chunk;
+    u64 lo, hi;
+};
+template <class P>
+__device__ __forceinline__ SibUnit sib_unit(const Fd2Args &a) {
+    const bool edge = blockIdx.x >= a.sib_blocks;
+    const u32 sunit = (edge ? blockIdx.x - a.sib_blocks : blockIdx.x) * P::WG + threadIdx.x;
+    const u32 upb = edge ? 1u : a.sib_upb;
+    SibUnit u;
+    u.active = sunit < (edge ? a.edge_units : a.sib_units);
+    u.chunk = edge ? a.edge_chunk : a.sib_chunk;
+    const u32 q = sunit / upb, k = sunit - q * upb;
+    u.lo = edge ? a.edge_lo : a.sib_lo;
+    u.hi = edge ? a.edge_hi : a.sib_hi;
+    add_u128(u.lo, u.hi, (u64)q * ((u64)P::SIB * P::B * P::B) + (u64)k * u.chunk);
+    return u;
+}
+
+// Histogram / near-miss record of sibling j's number at step i (mask m).
+template <class P>
+__device__ __forceinline__ void sib_count(const u32 (&m)[P::MW], int j, u32 i, const unsigned char *smem,
+                                          const Fd2Args &a, u32 hbase, u32 hinc, u32 *outl, u32 cutoff,
+                                          const NumOut &out) {
+    u32 uw = bcnt_acc(m[0], (u32)(-P::W0));
+#pragma unroll
+    for (int w = 1; w < P::MW; w++) uw += __popc(m[w]);
+    if (uw < (u32)P::W) {
+        atomicAdd((u32 *)(smem + uw * (P::HROW * 4) + hbase), hinc);
+    } else {
+        const u32 u = uw + P::W0;
+        atomicAdd(&outl[u], 1u);
+        if (u > cutoff) {
+            const SibUnit su = sib_unit<P>(a);
+            u64 lo = su.lo, hi = su.hi;
+            add_u128(lo, hi, (u64)j * ((u64)P::B * P::B) + i);
+            u32 pos = atomicAdd(out.count, 1u);
+            if (pos < out.cap) {
+                out.n[2 * (u64)pos] = lo;
+                out.n[2 * (u64)pos + 1] = hi;
+                out.u[pos] = u;
+            }
+        }
+    }
+}
+
+// walk_sib, pipelined (Cfg::LG >= 100): a step issues the shared lookups and
+// sibling 0's, computes the shared limb's carries (they need only the
+// low-digit entry) while those are in flight, issues sibling 1's, and then
+// per sibling j: consumes its lookups, counts its number, steps its upper
+// limbs and issues sibling j + 2's.  Two siblings' lookups are in flight
+// while the VALU works, so the lookups' latency hides behind arithmetic at 4
+// waves per SIMD (scheduling barriers pin the order).
+template <class P>
+__device__ __forceinline__ void walk_sib_pipe(State<P> (&st)[P::SIB], const unsigned char *smem, const Fd2Args &a,
+                                              u32 chunk, u32 hbase, u32 hinc, u32 *outl, u32 cutoff,
+                                              const NumOut &out) {
+    constexpr int L = P::LO;
+    constexpr int M = P::SIB;
+#pragma unroll
+    for (int j = 0; j < M; j++) sib_hi<P>(st[j], j, smem);
+    for (u32 i = 0; i < chunk; i++) {
+        SibLook<P> e[M];
+        // shared lookups (limb 0 of S and C, limb L of S and C) and sibling 0's
+        const uint2 vlo = *(const uint2 *)(smem + P::TL + st[0].r8);
+        uint2 vs, vc;
+        u32 mv[P::MW] = {};
+        if (P::vd_s(L)) or_valu<P>(st[0].S[L] - P::EBT, mv);
+        else vs = *(const uint2 *)(smem + (P::TB - (int)P::EBT) + st[0].S[L]);
+        if (P::vd_c(L)) or_valu<P>(st[0].C[L], mv);
+        else vc = *(const uint2 *)(smem + P::TB + st[0].C[L]);
+        sib_issue<P>(st[0], smem, e[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        // the shared limb's step (needs only the low-digit entry's carries)
+        const u32 w1 = vlo.y;
+        u32 cC, cS;
+        sib_shared_step<P>(st[0], w1, cC, cS);
+        if (M > 1) sib_issue<P>(st[1], smem, e[1]);
+        __builtin_amdgcn_sched_barrier(0);
+        u32 m0[P::MW];
+        bool topS[M], topC[M];
+        bool any = w1 >= P::FLAG_D1;
+#pragma unroll
+        for (int j = 0; j < M; j++) {
+            if (j == 0) {
+                m0[0] = vlo.x | mv[0] | (P::vd_s(L) ? 0u : vs.x) | (P::vd_c(L) ? 0u : vc.x);
+                m0[1] = (vlo.y & P::DMASK) | mv[1] | (P::vd_s(L) ? 0u : vs.y) | (P::vd_c(L) ? 0u : vc.y);
+            }
+            u32 m[P::MW];
+#pragma unroll
+            for (int w = 0; w < P::MW; w++) m[w] = m0[w] | st[j].hi[w];
+            sib_consume<P>(st[j], e[j], m);
+            sib_count<P>(m, j, i, smem, a, hbase, hinc, outl, cutoff, out);
+            any |= sib_upper_step<P>(st[j], cC, cS, topS[j], topC[j]);
+            if (j + 2 < M) sib_issue<P>(st[j + 2], smem, e[j + 2]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (any) rare_sib<P>(st, smem, w1 & P::FLAG_D1, w1 & P::FLAG_N3, topS, topC);
+    }
+}
+
+template <class P>
+__device__ __forceinline__ void walk_sib(State<P> (&st)[P::SIB], const unsigned char *smem, const Fd2Args &a,
+                                         u32 chunk, u32 hbase, u32 hinc, u32 *outl, u32 cutoff, const NumOut &out) {
+    if constexpr (P::LG >= 100) {
+        walk_sib_pipe<P>(st, smem, a, chunk, hbase, hinc, outl, cutoff, out);
+        return;
+    }
+    constexpr int L = P::LO;
+#pragma unroll
+    for (int j = 0; j < P::SIB; j++) sib_hi<P>(st[j], j, smem);
+    const u32 r80 = st[0].r8;
+    for (u32 i = 0; i < chunk; i++) {
+        // shared: limb 0 of S and C (low-digit entry) and limb 1 of both
+        u32 m0[P::MW];
+        const uint2 v = *(const uint2 *)(smem + P::TL + st[0].r8);
+        const u32 w1 = v.y;
+        m0[0] = v.x;
+        m0[1] = v.y & P::DMASK;
+        or_limb<P>(st[0], smem, true, L, m0);
+        or_limb<P>(st[0], smem, false, L, m0);
+#pragma unroll
+        for (int j = 0; j < P::SIB; j++) {
+            u32 m[P::MW];
+#pragma unroll
+            for (int w = 0; w < P::MW; w++) m[w] = m0[w] | st[j].hi[w];
+#pragma unroll
+            for (int q = L + 1; q < P::SL; q++) {
+                or_limb<P>(st[j], smem, true, q, m);
+                if (P::LG > 1 && (q - L) % P::LG == 0) lookup_group_end<P>(m);
+            }
+#pragma unroll
+            for (int q = L + 1; q < P::CL; q++) {
+                or_limb<P>(st[j], smem, false, q, m);
+                if (P::LG > 1 && (P::SL - L - 1 + q - L) % P::LG == 0) lookup_group_end<P>(m);
+            }
+            // a group per sibling: its loaded words are dead before the next
+            // sibling's lookups issue (bounds the VGPRs in flight)
+            if (P::LG) lookup_group_end<P>(m);
+            u32 uw = bcnt_acc(m[0], (u32)(-P::W0));
+#pragma unroll
+            for (int w = 1; w < P::MW; w++) uw += __popc(m[w]);
+            if (uw < (u32)P::W) {
+                atomicAdd((u32 *)(smem + uw * (P::HROW * 4) + hbase), hinc);
+            } else {
+                const u32 u = uw + P::W0;
+                atomicAdd(&outl[u], 1u);
+                if (u > cutoff) {
+                    const SibUnit su = sib_unit<P>(a);
+                    u64 lo = su.lo, hi = su.hi;
+                    add_u128(lo, hi, (u64)j * ((u64)P::B * P::B) + (st[0].r8 - r80) / P::ES);
+                    u32 pos = atomicAdd(out.count, 1u);
+                    if (pos < out.cap) {
+                        out.n[2 * (u64)pos] = lo;
+                        out.n[2 * (u64)pos + 1] = hi;
+                        out.u[pos] = u;
+                    }
+                }
+            }
+        }
+        step_sib<P>(st, smem, w1);
     }
 }
 
@@ -1114,13 +1595,17 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
     const u32 tid = threadIdx.x;
     const NumOut out = a.out;
     const u32 cutoff = a.cutoff;
-    // main part or tail part of the launch (workgroup-uniform)
-    const bool main_part = blockIdx.x < a.main_blocks;
+    // sibling parts (Cfg::SIB), then the main part and the tail part of the
+    // launch (workgroup-uniform)
+    const u32 sib_end = P::SIB > 1 ? a.sib_blocks + a.edge_blocks : 0u;
+    const bool sib_part = P::SIB > 1 && blockIdx.x < sib_end;
+    const u32 bid = blockIdx.x - sib_end;
+    const bool main_part = bid < a.main_blocks;
     const u64 start_lo = main_part ? a.start_lo : a.tail_lo;
     const u64 start_hi = main_part ? a.start_hi : a.tail_hi;
     const u32 nunits = main_part ? a.nunits : a.tail_count;
     const u32 chunk = main_part ? a.chunk : 1u;
-    const u32 blk = main_part ? blockIdx.x : blockIdx.x - a.main_blocks;
+    const u32 blk = main_part ? bid : bid - a.main_blocks;
     FD2_STAMP(a, 0);  // start
 
     // The tables (built once per device and base in global memory,
@@ -1171,21 +1656,50 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
     } else {
         add_u128(n0_lo, n0_hi, (u64)unit * chunk);
     }
+    // Window counters: row u - W0, column tid mod HROW (u16 halves / u8 quarters).
+    const u32 hbase = P::HB + tid % P::HROW * 4;
+    // (HROW is a multiple of 64: the increment is wave-uniform, an SGPR)
+    static_assert(P::HROW % 64 == 0, "window row of whole waves");
+    const u32 hinc = __builtin_amdgcn_readfirstlane(1u << (32 / P::HQ * (tid / P::HROW)));
+    u32 probe_acc = 0;
+    // Sibling lanes (workgroup-uniform): the sibling state is built, waited
+    // for and walked on its own path, so its registers never overlap the
+    // regular path's (one State live at the barrier, not M + 1).
+    bool sib_done = false;
+    if constexpr (P::SIB > 1) {
+        if (sib_part) {
+            State<P> sst[P::SIB];
+            const SibUnit su = sib_unit<P>(a);
+            if (su.active) {
+#pragma unroll
+                for (int j = 0; j < P::SIB; j++) {
+                    u64 lo = su.lo, hi = su.hi;
+                    add_u128(lo, hi, (u64)j * ((u64)P::B * P::B));
+                    init<P>(sst[j], lo, hi);
+                    sib_park<P>(sst[j], j, smem);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (su.active) walk_sib<P>(sst, smem, a, su.chunk, hbase, hinc, outl, cutoff, out);
+            sib_done = true;
+        }
+    }
     State<P> st;
-    if (active) init<P>(st, n0_lo, n0_hi);
+    if (!sib_done && active) init<P>(st, n0_lo, n0_hi);
     // The table DMA must have landed before any wave reads LDS: wait for it
     // explicitly (a workgroup barrier alone need not imply vmcnt(0)), then
     // the barrier.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (!sib_done) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
     FD2_STAMP(a, 1);  // state built, tables in LDS
-
-    // Window counters: row u - W0, column tid mod HROW (u16 halves / u8 quarters).
-    const u32 hbase = P::HB + tid % P::HROW * 4;
-    const u32 hinc = 1u << (32 / P::HQ * (tid / P::HROW));
-    u32 probe_acc = 0;
     FD2_STAMP(a, 2);  // (the cached mask is built inside walk_chunk)
-    if constexpr (!P::PERS) {
+    if constexpr (P::SIB > 1) {
+        if (!sib_done && active)
+            walk_chunk<P>(st, smem, chunk, n0_lo, n0_hi, hbase, hinc, outl, cutoff, out, probe_acc);
+    } else if constexpr (!P::PERS) {
         if (active) {
             walk_chunk<P>(st, smem, chunk, n0_lo, n0_hi, hbase, hinc, outl, cutoff, out, probe_acc);
         }
@@ -1266,7 +1780,123 @@ fd2_kernel(Fd2Args a) {
 }
 
 template <class P>
+static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Lane stride from a bank-conflict model.  A wave's lanes sit `L` numbers
+// apart (one chunk each), so the value of a HIGH limb across the lanes is an
+// arithmetic progression whose step is f'(n) L / B^q (f = n^2, n^3).  A
+// table lookup costs, per pass of 32 lanes (8-byte entries) or 16 lanes
+// (16-byte entries), the largest number of distinct entries that share a
+// bank slot (entry mod 32 / mod 16): 1-2 for a progression with an odd step,
+// up to 32 for a step that is a multiple of 32 -- e.g. b40's top C limb
+// steps ~32 per lane at L = 125 from the range start (modelled 91 against
+// 63 LDS cycles per wave-step, measured 2.35 against 1.86 ms per 1e9 in the
+// sibling kernel), and L = 81 hits the same 10 % into the range (2.37 vs
+// 1.90 ms; profiles/r05/sib_chunk_sweep.log).  The low limbs' values are
+// effectively random whatever L is, so the model counts only the limbs
+// whose value f / B^q stays below 2^60 (long double keeps their integer
+// part), at a few points of the segment and of the chunk, and the launch
+// takes the candidate stride with the smallest modelled cost.
+// ---------------------------------------------------------------------------
+// Cost of one lookup pass (`slots` lanes on `slots` bank slots) whose lane
+// values are floor(a + d l) mod B, as a function of the step d at a
+// resolution of 1/64, averaged over the offset a: max distinct values per
+// slot.  The pattern of slots depends on d mod slots, but whether lanes
+// share a value (a broadcast, free) only on d itself, so the table covers
+// d in [0, 2 slots): steps >= slots are looked up at slots + d mod slots.
+// Simulated once per process.
+static const std::vector<float> &progression_cost(int slots) {
+    static std::mutex mu;
+    static std::map<int, std::vector<float>> tab;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = tab.find(slots);
+    if (it != tab.end()) return it->second;
+    std::vector<float> t((size_t)slots * 128);
+    for (size_t k = 0; k < t.size(); k++) {
+        const double d = (double)k / 64;
+        double sum = 0;
+        for (int ai = 0; ai < 16; ai++) {
+            const double a = ai / 16.0 + 0.03125;
+            int cnt[32] = {}, seen[32][32];
+            int best = 0;
+            for (int l = 0; l < slots; l++) {
+                const long v = (long)std::floor(a + d * l) + 1000000L * slots;  // >= 0
+                const int sl = (int)(v % slots);
+                bool dup = false;
+                for (int q = 0; q < cnt[sl]; q++) dup |= seen[sl][q] == (int)(v % 100000);
+                if (!dup) seen[sl][cnt[sl]++] = (int)(v % 100000);
+                best = std::max(best, cnt[sl]);
+            }
+            sum += best;
+        }
+        t[k] = (float)(sum / 16);
+    }
+    return tab.emplace(slots, std::move(t)).first->second;
+}
+
+// Modelled LDS cycles of a wave-step's lookups of the limbs whose lane
+// values progress (the high looked-up limbs of S = n^2 and C = n^3 from
+// first_limb on, where the lanes' quadratic drift stays under half a unit)
+// at lane stride L, averaged over the segment's start, middle and end.  The
+// other limbs' values are effectively random whatever L is and are left out.
+template <class P>
+static double lookup_conflict_model(long double n0, long double span, u64 L, int first_limb) {
+    constexpr int SLOTS = P::ES == 16 ? 16 : 32;
+    constexpr int NPASS = 64 / SLOTS;
+    const std::vector<float> &tab = progression_cost(SLOTS);
+    double cost = 0;
+    for (int pt = 0; pt < 3; pt++) {
+        const long double n = n0 + span * (long double)pt / 2;
+        const long double w = (long double)L * 64;  // the wave's span of n
+        for (int cube = 0; cube < 2; cube++) {
+            const int hi = cube ? P::CL : P::SL;
+            long double bq = 1;
+            for (int q = 0; q < first_limb; q++) bq *= (long double)P::B;
+            for (int q = first_limb; q < hi; q++, bq *= (long double)P::B) {
+                if (cube ? P::vd_c(q) : P::vd_s(q)) continue;
+                const long double f1 = cube ? 3 * n * n : 2 * n;   // f'(n)
+                const long double f2 = cube ? 6 * n : 2;           // f''(n)
+                if (f2 * w * w / 2 / bq >= 0.5L) continue;         // drifting: effectively random
+                const long double d = f1 * (long double)L / bq;    // lane step in limb units
+                const long double r = d < SLOTS ? d : SLOTS + fmodl(d, (long double)SLOTS);
+                cost += NPASS * tab[std::min<size_t>(tab.size() - 1, (size_t)(r * 64))];
+            }
+        }
+    }
+    return cost / 3;
+}
+
+// The odd stride in [lo, hi] with the lowest modelled cost at the segment
+// [start, start + count); among the strides within `tol` modelled cycles of
+// the best, the one closest to target (a lane's init amortises over its
+// chunk).  A few hundred table lookups: cheap enough for every launch.
+template <class P>
+static u64 pick_lane_stride(u128 start, u64 count, u64 lo, u64 hi, u64 target, int first_limb,
+                            double tol = 0.5) {
+    const long double n0 = (long double)start;
+    double cost[512];
+    int nc = 0;
+    double min_cost = 1e30;
+    for (u64 L = lo | 1; L <= hi && nc < 512; L += 2, nc++) {
+        cost[nc] = lookup_conflict_model<P>(n0, (long double)count, L, first_limb);
+        min_cost = std::min(min_cost, cost[nc]);
+    }
+    u64 best = target | 1, best_d = ~0ull;
+    nc = 0;
+    for (u64 L = lo | 1; L <= hi && nc < 512; L += 2, nc++) {
+        const u64 d = L > target ? L - target : target - L;
+        if (cost[nc] <= min_cost + tol && d < best_d) {
+            best = L;
+            best_d = d;
+        }
+    }
+    return best;
+}
+
+template <class P>
 static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s) {
+    if constexpr (P::SIB > 1) return launch_sib<P>(p, num_cus, s);
     auto kern = fd2_kernel<P>;
     // Occupancy is a property of the code object: queried once per
     // instantiation (a runtime call per launch is host latency on small fields).
@@ -1332,6 +1962,11 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
             // b80 1e9 at chunk 2544 took 11.8 ms, at 2545 9.3.
             if (chunk > 1 && (P::LSD ? chunk % 2 == 0 : chunk % 16 == 0)) chunk++;
             if (chunk > P::B) chunk = P::B % 2 ? P::B : P::B - 1;
+            // (The bank-conflict model that picks the sibling kernel's lane
+            // stride, pick_lane_stride, did not help the persistent-grid
+            // kernels of the wider bases: re-picking their chunk where it
+            // modelled a pathology moved b45..80 by -5 .. +9 %,
+            // profiles/r05/model_sweep.log, model_sweep2.log.)
             if (P::HQ == 4 && chunk > 255) return hipErrorInvalidValue;
             nunits = cnt / chunk;
             tail = cnt - nunits * chunk;  // < chunk <= B: one number per lane
@@ -1390,12 +2025,120 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
 }
 
 
-}  // namespace fd2
-}  // namespace nice
-
-namespace nice {
-namespace fd2 {
-
+// Sibling-lane launches (Cfg::SIB = M > 1).  A segment [a, a + count) is
+// Q super-blocks of M B^2 numbers plus a remainder R < M B^2.  Super-block q
+// is walked by units (q, k): a lane takes the numbers a + q M B^2 + j B^2 +
+// k L + i (j < M, i < L) for k < B^2 / L, and the last L' = B^2 mod L (or L)
+// numbers of each B^2 block are the edge units (one per super-block, chunk
+// L'); the remainder R runs as the regular main + tail parts of the same
+// launch.  Launches are split so unit counts stay 32-bit; the field's finish
+// rides on the last.
+template <class P>
+static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s) {
+    auto kern = fd2_kernel<P>;
+    static const int per_cu_q = [&] {
+        int v = 0;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, (const void *)kern, P::WG, 0) == hipSuccess
+                   ? v : -1;
+    }();
+    if (per_cu_q < 0) return hipErrorInvalidDeviceFunction;
+    const int per_cu = per_cu_q < 1 ? 1 : per_cu_q;
+    constexpr u64 D = (u64)P::B * P::B, SB = (u64)P::SIB * D;
+    // too short for the sibling walk to pay: the same base without siblings
+    if (p.count < 4 * SB) return launch_cfg<typename P::NoSib>(p, num_cus, s);
+    if (p.cutoff + 1 < (u32)(P::W0 + P::W)) return hipErrorInvalidValue;
+    const u64 lanes = (u64)num_cus * per_cu * P::WG;
+    const uint4 *tabs = nullptr;
+    hipError_t e = fd2_tables<P>(s, &tabs);
+    if (e != hipSuccess) return e;
+    // Sibling chunk L: odd, so limb 0's low-digit lookups of a half-wave hit
+    // 32 distinct bank pairs (as launch_cfg's chunks).
+    const u128 seg_start = ((u128)p.start_hi << 64) | p.start_lo;
+    u64 L = probe_knob("NICE_FD2_SIBCHUNK", 0);
+    if (!L) L = pick_lane_stride<P>(seg_start, p.count, P::TCHUNK * 3 / 4, P::TCHUNK * 3 / 2, P::TCHUNK, P::LO + 1);
+    if (L % 2 == 0) L++;
+    if (L > D / 4) L = (D / 4) | 1;
+    const u64 U = (D + L - 1) / L, r = D - (U - 1) * L;
+    const bool has_edge = r != L;
+    const u64 upb = has_edge ? U - 1 : U;
+    // the lanes' u16 window counters hold M L numbers
+    if ((u64)P::SIB * L > 65535) return hipErrorInvalidValue;
+    // Launch bound: unit counts in 32 bits and, as launch_cfg's, 60 000
+    // numbers per resident lane -- counted at the regular kernel's 2048 lanes
+    // per CU, so a b40 launch still takes up to 3.1e10 numbers whatever the
+    // sibling kernel's own occupancy.
+    const u64 qmax = std::max<u64>(1, std::min<u64>(0xffffffffull / upb, ((u64)num_cus * 2048 * 60000ull) / SB));
+    DetailedLaunch q = p;
+    u64 left = p.count;
+    const u64 tchunk = probe_knob("NICE_FD2_TCHUNK", (u64)P::TCHUNK);
+    while (left) {
+        u64 Q = left / SB, cnt = left;
+        if (Q > qmax) {
+            Q = qmax;
+            cnt = Q * SB;
+        }
+        // regular remainder (the last launch only): rounds of one chunk per lane
+        const u64 R = cnt - Q * SB;
+        u64 chunk = 1, nunits = 0, tail = 0;
+        if (R) {
+            u64 rounds = (R + tchunk * lanes - 1) / (tchunk * lanes);
+            if (rounds < 1) rounds = 1;
+            chunk = (R + rounds * lanes - 1) / (rounds * lanes);
+            if (chunk < 4) chunk = R < 4 ? R : 4;
+            if (chunk < 1) chunk = 1;
+            if (chunk > 1 && chunk % 2 == 0) chunk++;
+            if (chunk > P::B) chunk = P::B % 2 ? P::B : P::B - 1;
+            nunits = R / chunk;
+            tail = R - nunits * chunk;
+        }
+        Fd2Args a{};
+#ifdef NICE_PROBES
+        a.stamps = g_stamps;
+#endif
+        a.sib_lo = q.start_lo;
+        a.sib_hi = q.start_hi;
+        a.sib_chunk = (u32)L;
+        a.sib_upb = (u32)upb;
+        a.sib_units = (u32)(Q * upb);
+        a.sib_blocks = (u32)((Q * upb + P::WG - 1) / P::WG);
+        a.edge_lo = q.start_lo;
+        a.edge_hi = q.start_hi;
+        add_u128(a.edge_lo, a.edge_hi, upb * L);
+        a.edge_chunk = (u32)r;
+        a.edge_units = has_edge ? (u32)Q : 0u;
+        a.edge_blocks = has_edge ? (u32)((Q + P::WG - 1) / P::WG) : 0u;
+        a.start_lo = q.start_lo;
+        a.start_hi = q.start_hi;
+        add_u128(a.start_lo, a.start_hi, Q * SB);
+        a.tail_lo = a.start_lo;
+        a.tail_hi = a.start_hi;
+        add_u128(a.tail_lo, a.tail_hi, nunits * chunk);
+        a.nunits = (u32)nunits;
+        a.chunk = (u32)chunk;
+        a.tail_count = (u32)tail;
+        a.main_blocks = (u32)((nunits + P::WG - 1) / P::WG);
+        a.cutoff = q.cutoff;
+        a.ncopies = q.hist_copies;
+        a.wave_cap = 0;
+        a.hist = q.hist;
+        a.out = q.out;
+        a.tabs = tabs;
+        a.fin = left == cnt ? q.fin : FieldFinish{nullptr, nullptr};
+        const u64 grid = (u64)a.sib_blocks + a.edge_blocks + a.main_blocks + (tail + P::WG - 1) / P::WG;
+#ifdef NICE_PROBES
+        {
+            const u64 v[6] = {grid, (u64)P::WG, L, Q * upb, R, (u64)per_cu};
+            for (int k = 0; k < 6; k++) g_last_launch[k] = v[k];
+        }
+#endif
+        hipLaunchKernelGGL(kern, dim3((u32)grid), dim3(P::WG), 0, s, a);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (p.launches) ++*p.launches;
+        add_u128(q.start_lo, q.start_hi, cnt);
+        left -= cnt;
+    }
+    return hipSuccess;
+}
 
 }  // namespace fd2
 }  // namespace nice

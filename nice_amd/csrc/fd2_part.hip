@@ -88,6 +88,24 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
             default: break;
             }
         }
+        // Sibling lanes (Cfg::SIB) A/B: NICE_FD2_SIB = 1: the round-4 kernel
+        // (no siblings); 31 / 131 / 132 / 141 / 142 / 143 / 144 / 121: M = 3
+        // or 2 siblings at the VALU decode / lookup grouping in the cases
+        if constexpr (B_ == 40) {
+            constexpr int VL = valu_limbs_big(B_, ND_, NE_);
+            switch ((int)probe_knob("NICE_FD2_SIB", 0)) {
+            case 1: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, big_wg(B_), VL>>(p, num_cus, s);
+            case 31: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, VL, 1, 0, 3>>(p, num_cus, s);
+            case 131: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, 0, 1, 0, 3>>(p, num_cus, s);
+            case 132: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, 0, 100, 0, 3>>(p, num_cus, s);
+            case 141: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, 4097, 1, 0, 3>>(p, num_cus, s);
+            case 142: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, 4097, 100, 0, 3>>(p, num_cus, s);
+            case 143: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, 4098, 1, 0, 3>>(p, num_cus, s);
+            case 144: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, 4113, 1, 0, 3>>(p, num_cus, s);
+            case 121: return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, 4097, 1, 0, 2>>(p, num_cus, s);
+            default: break;
+            }
+        }
         // Persistent grid A/B (NICE_FD2_PERS = 1: on, 2: off; 3 / 4: 1024-thread
         // workgroups with / without it, where the LDS and VGPRs allow one)
         if constexpr (waves_at(B_, 1024) >= 4) {
@@ -122,6 +140,17 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
             }
         }
 #endif
+        // b40 fields >= 1e7: three sibling lanes (Cfg::SIB, fd2_kernel.hpp):
+        // on the first limb layout (the range's first ~29 %, the benchmark
+        // fields) pipelined with the lowest C limb above the shared one
+        // decoded by VALU, elsewhere per-sibling lookup groups, no VALU decode
+        // (profiles/r05/sib_sweep_range.log)
+        if constexpr (B_ == 40) {
+            if (!wg512) {
+                if constexpr (ND_ == 4) return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, 4097, 100, 0, 3>>(p, num_cus, s);
+                else return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, 0, 1, 0, 3>>(p, num_cus, s);
+            }
+        }
         // (the LSDX bases' tables leave room for one workgroup per CU: 1024
         // threads for every field size, 4 waves per SIMD instead of 2)
         // (fields of >= 1e7 take valu_limbs_big: see there)

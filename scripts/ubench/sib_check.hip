@@ -1,0 +1,96 @@
+// Standalone A/B of one FD kernel configuration against the production b40
+// configuration on the same field (no library, no finish): histograms summed
+// over the copies on the host, near-miss counts compared, times printed.
+// Build (CPU side):  hipcc --offload-arch=gfx950 -O3 -std=c++17 -DXM=2 -DXWG=768
+//   -DXVD=2049 -DXLG=-1 scripts/ubench/sib_check.hip -o scripts/ubench/sib_check
+// Run: sib_check START COUNT [REPS]
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../../nice_amd/csrc/fd2_kernel.hpp"
+
+using namespace nice;
+using namespace nice::fd2;
+#ifndef XLG
+#define XLG -1
+#endif
+using Ref = Cfg<40, 4, 8, 5, 0, 1024, 2049>;
+using Var = Cfg<40, 4, 8, 5, 0, XWG, XVD, XLG, 0, XM>;
+
+template <class P>
+static double run(u64 start, u64 count, std::vector<u64> &hist, u32 &nmiss, int reps) {
+    u64 *d_hist;
+    u32 *d_count;
+    u64 *d_n;
+    u32 *d_u;
+    hipMalloc(&d_hist, kHistCopies * 129 * 8);
+    hipMalloc(&d_count, 4);
+    hipMalloc(&d_n, (1 << 20) * 16);
+    hipMalloc(&d_u, (1 << 20) * 4);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    int cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    double best = 1e30;
+    for (int r = 0; r < reps; r++) {
+        hipMemset(d_hist, 0, kHistCopies * 129 * 8);
+        hipMemset(d_count, 0, 4);
+        DetailedLaunch p{};
+        p.start_lo = start;
+        p.count = count;
+        p.base = 40;
+        p.cutoff = 36;
+        p.hist = d_hist;
+        p.hist_copies = kHistCopies;
+        p.out = NumOut{d_n, d_u, d_count, 1u << 20};
+        p.fin = FieldFinish{nullptr, nullptr, 0};
+        hipEventRecord(e0, 0);
+        hipError_t e = launch_cfg<P>(p, cus, 0);
+        hipEventRecord(e1, 0);
+        if (e != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            printf("launch failed: %s\n", hipGetErrorString(e));
+            exit(1);
+        }
+        float ms = 0;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (ms < best) best = ms;
+    }
+    std::vector<u64> h(kHistCopies * 129);
+    hipMemcpy(h.data(), d_hist, h.size() * 8, hipMemcpyDeviceToHost);
+    hipMemcpy(&nmiss, d_count, 4, hipMemcpyDeviceToHost);
+    hist.assign(129, 0);
+    for (u32 c = 0; c < kHistCopies; c++)
+        for (int b = 0; b < 129; b++) hist[b] += h[c * 129 + b];
+    hipFree(d_hist);
+    hipFree(d_count);
+    hipFree(d_n);
+    hipFree(d_u);
+    return best;
+}
+
+int main(int argc, char **argv) {
+    const u64 start = argc > 1 ? strtoull(argv[1], 0, 10) : 1916284264916ull;
+    const u64 count = argc > 2 ? strtoull(argv[2], 0, 10) : 100000000ull;
+    const int reps = argc > 3 ? atoi(argv[3]) : 3;
+    std::vector<u64> h0, h1;
+    u32 m0 = 0, m1 = 0;
+    const double t0 = run<Ref>(start, count, h0, m0, reps);
+    const double t1 = run<Var>(start, count, h1, m1, reps);
+    u64 s0 = 0, s1 = 0;
+    int bad = 0;
+    for (int b = 0; b < 129; b++) {
+        s0 += h0[b];
+        s1 += h1[b];
+        if (h0[b] != h1[b]) {
+            if (bad < 8) printf("bin %d: ref %llu var %llu\n", b, (unsigned long long)h0[b], (unsigned long long)h1[b]);
+            bad++;
+        }
+    }
+    printf("M=%d WG=%d VD=%d LG=%d start=%llu count=%llu: ref %.1f us var %.1f us, sums %llu %llu, "
+           "near-miss %u %u, %s\n",
+           XM, XWG, XVD, XLG, (unsigned long long)start, (unsigned long long)count, t0 * 1e3, t1 * 1e3,
+           (unsigned long long)s0, (unsigned long long)s1, m0, m1, bad || m0 != m1 ? "MISMATCH" : "match");
+    return bad || m0 != m1;
+}

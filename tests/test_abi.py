@@ -267,20 +267,25 @@ def test_product_library_has_no_probe_kernels():
     cfgs = [[int(x) for x in m.split(", ")]
             for m in re.findall(r"fd2_kernel<nice::fd2::Cfg<(-?\d+(?:, -?\d+)*)>", syms)]
     assert cfgs, "no fd2 kernels found"
-    # Cfg<BASE, ND, NE, NE2, PROBE, WG, VD, LG, PERS>
-    assert all(len(c) == 9 for c in cfgs), cfgs[:3]
+    # Cfg<BASE, ND, NE, NE2, PROBE, WG, VD, LG, PERS, SIB>
+    assert all(len(c) == 10 for c in cfgs), cfgs[:3]
     assert all(c[4] == 0 for c in cfgs), "probe instantiation in the product library"
     # neither the split b64 + u16 table layout (VD & 512) nor a forced lookup
     # grouping (the per-base default is -1) is a product variant; PERS is the
-    # per-base default (-1) or the rounds fallback of a persistent kernel (0)
-    assert all(c[6] & 512 == 0 and c[7] == -1 and c[8] in (-1, 0) for c in cfgs), \
-        "probe variant in the product library"
+    # per-base default (-1) or the rounds fallback of a persistent kernel (0).
+    # The sibling-lane kernels (SIB > 1, b40 only) name their walk explicitly:
+    # LG 1 (per-sibling lookup groups) or 100 (the software-pipelined walk)
+    for c in cfgs:
+        assert c[6] & 512 == 0 and c[8] in (-1, 0), c
+        assert c[7] == -1 if c[9] <= 1 else (c[0] == 40 and c[9] == 3 and c[7] in (1, 100)), c
+    assert any(c[9] == 3 for c in cfgs), "no sibling-lane kernel"
     assert "detailed_fd_kernel" not in syms
     with open(_lib.LIB_PATH, "rb") as f:
         blob = f.read()
     for knob in (b"NICE_FD2_PROBE", b"NICE_MSD_PROBE", b"NICE_FD_VARIANT", b"NICE_FD2_TCHUNK",
                  b"NICE_FD2_MINCHUNK", b"NICE_FD2_WG512", b"NICE_MSD_TRACE", b"NICE_FD2_LG",
-                 b"NICE_FD2_COPIES", b"NICE_FD2_VD", b"NICE_FD2_PERS"):
+                 b"NICE_FD2_COPIES", b"NICE_FD2_VD", b"NICE_FD2_PERS", b"NICE_FD2_SIB",
+                 b"NICE_FD2_NOMODEL"):
         assert knob not in blob, knob
 
 

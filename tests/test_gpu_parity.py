@@ -1257,3 +1257,38 @@ def test_eight_shard_context():
             assert got_n[k] == [n for n, _ in want_n.nice_numbers]
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("frac", [0.0, 0.1, 0.2926, 0.45, 0.97])
+def test_sibling_kernel_equals_small_fields(ctx, frac):
+    """b40 fields of >= 1e7 (and >= 4 super-blocks of 3 x 40^4 numbers) run
+    the sibling-lane kernel (Cfg::SIB = 3, fd2_kernel.hpp: a lane steps n,
+    n + B^2 and n + 2 B^2 together, sharing limbs 0 and 1; super-blocks,
+    edge units where the lane stride does not divide B^2, and the regular
+    remainder in one launch; the lane stride from the bank-conflict model).
+    Fields below 1e7 run the round-4 kernel at 512 threads.  A field of
+    ragged size at several points of the range (0.2926: across the limb-count
+    cut at 2n + 1 = 40^8) must equal the sum of its sub-1e7 pieces, and every
+    near-miss must recompute by the oracle."""
+    r0, r1 = O.base_range(40)
+    s = r0 + int((r1 - r0) * frac) + 12345
+    n = 4 * 3 * 1600 ** 2 + 2_345_677  # 4 super-blocks + a remainder
+    if s + n > r1:
+        s = r1 - n
+    h, l = ctx.detailed_raw(s, s + n, 40)
+    assert sum(h) == n
+    piece = 9_000_001
+    hs, ls = [0] * len(h), []
+    a = s
+    while a < s + n:
+        b = min(s + n, a + piece)
+        hk, lk = ctx.detailed_raw(a, b, 40)
+        hs = [x + y for x, y in zip(hs, hk)]
+        ls += lk
+        a = b
+    assert h == hs and l == ls
+    assert all(O.num_unique_digits(m, 40) == u for m, u in l)
+    # a window of the same field against the oracle itself
+    want = O.process_range_detailed(s, s + 200_003, 40)
+    hw, lw = ctx.detailed_raw(s, s + 200_003, 40)
+    assert _dist(hw) == want.distribution and lw == want.nice_numbers
