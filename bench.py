@@ -99,7 +99,7 @@ def parse():
     return p.parse_args()
 
 
-PMC_BENCH_FILE = "profiles/r04/pmc_bench.json"
+PMC_BENCH_FILE = "profiles/r05/pmc_bench.json"
 
 
 def lib_sha16() -> str:
@@ -501,18 +501,25 @@ def main(args):
             line["roofline"]["hw_source"] = src
             line["roofline"]["hw_status"] = status
             if der is not None:
-                vb, lb = der.get("valu_busy"), der.get("lds_busy")
+                vb, lb = der.get("valu_issue_busy", der.get("valu_busy")), der.get("lds_busy")
                 line["roofline"]["traffic"] = der.get("traffic_bytes")
                 line["roofline"]["hw"] = {
-                    "valu_busy": vb, "lds_busy": lb,
+                    "valu_issue_busy": der.get("valu_issue_busy"), "valu_busy_counter": der.get("valu_busy"),
+                    "valu_cpi": der.get("valu_cpi"), "valu_cpi_source": der.get("valu_cpi_source"),
+                    "lds_busy": lb,
                     "lds_conflict_frac": der.get("lds_conflict_frac"),
                     "lds_cycles_per_instr": der.get("lds_cycles_per_instr"),
                     "valu_lane_ops_per_n": der.get("valu_lane_ops_per_n"),
                     "lds_instr_per_n": der.get("lds_instr_per_n"),
                     "kernel_cycles": der.get("kernel_cycles"),
-                    "note": "valu_busy = VALUBusy/100 (SQ_ACTIVE_INST_VALU / CUs / kernel cycles; it "
-                            "can pass 1 with the fast-issue integer ops, profiles/r01/"
-                            "isa_issue_rates_gfx950.log); lds_busy = SQ_LDS_IDX_ACTIVE / CUs / kernel "
+                    "note": "valu_issue_busy = SQ_INSTS_VALU x valu_cpi / (4 SIMDs x CUs x kernel "
+                            "cycles): the share of the kernel's SIMD cycles its VALU instructions "
+                            "occupy the issue port, valu_cpi = issue cycles per instruction of the "
+                            "hot loop's opcode mix at the measured gfx950 rates (valu_cpi_source; "
+                            "profiles/r01/isa_issue_rates_gfx950.log) -- <= 1 by construction; "
+                            "valu_busy_counter = VALUBusy/100 (SQ_ACTIVE_INST_VALU / CUs / kernel "
+                            "cycles), one count per instruction whatever its rate, so not a "
+                            "share and it can pass 1; lds_busy = SQ_LDS_IDX_ACTIVE / CUs / kernel "
                             "cycles (the CU's one LDS pipe; the counter matches the CU's s_memtime "
                             "span on the kernel's own index trace, profiles/r04/lds_trace.log); "
                             "both pipes near 1 = co-bound; lds_conflict_frac = SQ_LDS_BANK_CONFLICT / "

@@ -621,12 +621,10 @@ __device__ __forceinline__ void normalize(const A (&acc)[N], u32 (&out)[M]) {
     }
 }
 
-// Lane state at n (every limb but the cached mask, which needs the tables:
-// recompute_hi after them).
+// Radix-B digits X of n.
 template <class P>
-__device__ __forceinline__ void init(State<P> &st, u64 n_lo, u64 n_hi) {
+__device__ __forceinline__ void init_digits(u32 (&X)[P::NX], u64 n_lo, u64 n_hi) {
     constexpr u32 B = P::B;
-    u32 X[P::NX];
     if constexpr (P::N64) {
         // In-range n fits 64 bits (b40 < 2^43, b50 < 2^57): two radix-B digits
         // per u64 division by B^2, the rest in 32 bits.
@@ -655,6 +653,12 @@ __device__ __forceinline__ void init(State<P> &st, u64 n_lo, u64 n_hi) {
             X[j] = (u32)rem;
         }
     }
+}
+
+// Plain (unscaled, unbiased) limbs of S = n^2, C = n^3, D1 = 2n + 1 and
+// N3 = 3n + 1 from n's digits X, and the low-digit offsets.
+template <class P>
+__device__ __forceinline__ void init_plain(State<P> &st, const u32 (&X)[P::NX]) {
     // Column sums: at most min(NS, NX) products < B^2 plus a carry: 32 bits
     // (Cfg static_assert).
     using A = u32;
@@ -731,6 +735,12 @@ __device__ __forceinline__ void init(State<P> &st, u64 n_lo, u64 n_hi) {
             normalize<P>(acc, st.N3);
         }
     }
+}
+
+// Plain limbs -> the stepped representation (scaled by the entry stride,
+// biased; limb 0 from the low-digit table where there is one).
+template <class P>
+__device__ __forceinline__ void init_scale(State<P> &st) {
     if constexpr (P::LSD) st.S[0] = st.C[0] = st.D1[0] = st.N3[0] = 0;  // from the table
 #pragma unroll
     for (int i = 0; i < P::SL; i++) st.S[i] = (st.S[i] + P::BT) * P::ES;
@@ -740,6 +750,16 @@ __device__ __forceinline__ void init(State<P> &st, u64 n_lo, u64 n_hi) {
     for (int i = 0; i < P::ND; i++) st.D1[i] *= P::ES;
 #pragma unroll
     for (int i = 0; i < P::NN; i++) st.N3[i] = st.N3[i] * P::ES - (i < P::SL ? 3 * P::EBT : 0u);
+}
+
+// Lane state at n (every limb but the cached mask, which needs the tables:
+// recompute_hi after them).
+template <class P>
+__device__ __forceinline__ void init(State<P> &st, u64 n_lo, u64 n_hi) {
+    u32 X[P::NX];
+    init_digits<P>(X, n_lo, n_hi);
+    init_plain<P>(st, X);
+    init_scale<P>(st);
 }
 
 // +ES into scaled plain limbs [from, N) (rare path).
@@ -1153,6 +1173,9 @@ __device__ __forceinline__ u32 c_limb(State<P> &st, int i, u32 cC) {
     else if (i < P::SL) t -= 3 * P::EBT;
     if (i < P::SL) t = mad_u24<3>(st.S[i], t);
     else if (i < P::NS) t += st.S[i];
+    // (The scaled carry straight from one multiply-high, mulhi(t, ES MAGIC) &
+    // -ES, prices 18 cycles fewer per step in the issue budget but measured
+    // 0.6-2.2 % slower, interleaved A/B: profiles/r05/carry_c8_ab.log.)
     const u32 c = P::C1 ? __umulhi(t, P::MAGIC) : __umulhi(t / P::ES, P::MAGICB);
     st.C[i] = t - c * P::DC;
     return c * P::ES;
@@ -1186,6 +1209,44 @@ __device__ __forceinline__ void sib_hi(State<P> &st, int j, const unsigned char 
         or_plain<P>(smem, *cold_slot<P>(smem, j, k), P::CL + k == P::NC - 1 ? P::C_TOPD : 2, st.hi);
 }
 
+// Plain limbs of sibling j (n + j B^2) from sibling 0's plain limbs and n's
+// digits X: (n + j B^2)^2 = S + 2 j n B^2 + j^2 B^4 and (n + j B^2)^3 = C +
+// 3 j S B^2 + 3 j^2 n B^4 + j^3 B^6 -- column adds and one normalisation
+// instead of sibling j's own radix conversion and products (~1/3 of a
+// lane's init each).
+template <class P>
+__device__ __forceinline__ void sib_derive(State<P> &sj, const State<P> &s0, const u32 (&X)[P::NX], u32 j) {
+    {
+        u32 acc[P::NS];
+#pragma unroll
+        for (int t = 0; t < P::NS; t++)
+            acc[t] = s0.S[t] + (t >= 2 && t - 2 < P::NX ? 2 * j * X[t - 2] : 0u) + (t == 4 ? j * j : 0u);
+        normalize<P>(acc, sj.S);
+    }
+    {
+        u32 acc[P::NC];
+#pragma unroll
+        for (int t = 0; t < P::NC; t++)
+            acc[t] = s0.C[t] + (t >= 2 && t - 2 < P::NS ? 3 * j * s0.S[t - 2] : 0u) +
+                     (t >= 4 && t - 4 < P::NX ? 3 * j * j * X[t - 4] : 0u) + (t == 6 ? j * j * j : 0u);
+        normalize<P>(acc, sj.C);
+    }
+    {
+        u32 acc[P::ND];
+#pragma unroll
+        for (int t = 0; t < P::ND; t++) acc[t] = s0.D1[t] + (t == 2 ? 2 * j : 0u);
+        normalize<P>(acc, sj.D1);
+    }
+    {
+        u32 acc[P::NN];
+#pragma unroll
+        for (int t = 0; t < P::NN; t++) acc[t] = s0.N3[t] + (t == 2 ? 3 * j : 0u);
+        normalize<P>(acc, sj.N3);
+    }
+    sj.r8 = s0.r8;
+    sj.rc = s0.rc;
+}
+
 // Sibling state after init: cached S limbs to K form, cached C limbs to LDS.
 template <class P>
 __device__ __forceinline__ void sib_park(State<P> &st, int j, const unsigned char *smem) {
@@ -1199,23 +1260,20 @@ __device__ __forceinline__ void sib_park(State<P> &st, int j, const unsigned cha
 // siblings: the shared limb 1, then each sibling's upper limbs) and carries
 // out of each sibling's top stepped limbs (rare()'s work per sibling).
 template <class P>
-__device__ __forceinline__ void rare_sib(State<P> (&st)[P::SIB], const unsigned char *smem, u32 d1w, u32 n3w,
+__device__ __forceinline__ void rare_sib(State<P> (&st)[P::SIB], const unsigned char *smem,
                                       const bool (&cS)[P::SIB], const bool (&cC)[P::SIB]) {
     constexpr int L = P::LO;
-    if (d1w) {
-        const u32 v = st[0].D1[L] + P::ES;
-        const bool c = v >= P::ESB;
-        st[0].D1[L] = c ? 0u : v;
-        if (c)
+    // limb L of the shared D1 / N3 reached B (sib_shared_step stepped it):
+    // wrap it and carry into every sibling's limbs above
+    if (st[0].D1[L] >= P::ESB) {
+        st[0].D1[L] -= P::ESB;
 #pragma unroll
-            for (int j = 0; j < P::SIB; j++) carry_scaled<P>(st[j].D1, L + 1);
+        for (int j = 0; j < P::SIB; j++) carry_scaled<P>(st[j].D1, L + 1);
     }
-    if (n3w) {
+    {
         const u32 off1 = L < P::SL ? 3 * P::EBT : 0u;
-        const u32 v = st[0].N3[L] + off1 + P::ES;
-        const bool c = v >= P::ESB;
-        st[0].N3[L] = (c ? 0u : v) - off1;
-        if (c) {
+        if (st[0].N3[L] + off1 >= P::ESB) {
+            st[0].N3[L] -= P::ESB;
 #pragma unroll
             for (int j = 0; j < P::SIB; j++) {
                 u32 cc = 1;
@@ -1262,28 +1320,10 @@ __device__ __forceinline__ void step_sib(State<P> (&st)[P::SIB], const unsigned 
     constexpr u32 ES = P::ES;
     constexpr int L = P::LO;
     constexpr int CT = P::CL - 1, ST = P::SL - 1;
-    State<P> &s0 = st[0];
-    // shared limb L of C += 3S + N3 (old S) and of S += D1
-    u32 cC = __builtin_amdgcn_ubfe(w1, P::FC, P::FCW);
-    {
-        u32 t = P::TIGHT ? mad_u24<ES>(cC, s0.C[L]) : s0.C[L] + cC;
-        if (L < P::NN) t += s0.N3[L];
-        else t -= 3 * P::EBT;
-        t = mad_u24<3>(s0.S[L], t);
-        const u32 c = P::C1 ? __umulhi(t, P::MAGIC) : __umulhi(t / ES, P::MAGICB);
-        s0.C[L] = t - c * P::DC;
-        cC = c * ES;
-    }
-    u32 cS = __builtin_amdgcn_ubfe(w1, P::F0, P::F0W);
-    {
-        const u32 d = L < P::ND ? s0.D1[L] : 0u;
-        const u32 t = P::TIGHT ? mad_u24<ES>(cS, s0.S[L] + d) : s0.S[L] + d + cS;
-        cS = (t >> P::T) & ES;
-        s0.S[L] = t - cS * P::B;
-    }
-    s0.r8 += ES;
+    u32 cC, cS;
+    bool any;
+    sib_shared_step<P>(st[0], w1, cC, cS, any);
     bool topS[P::SIB], topC[P::SIB];
-    bool any = w1 >= P::FLAG_D1;
 #pragma unroll
     for (int j = 0; j < P::SIB; j++) {
         u32 c = cC;
@@ -1298,15 +1338,17 @@ __device__ __forceinline__ void step_sib(State<P> (&st)[P::SIB], const unsigned 
         topC[j] = st[j].C[CT] >= P::DC;
         any |= topS[j] | topC[j];
     }
-    if (any) rare_sib<P>(st, smem, w1 & P::FLAG_D1, w1 & P::FLAG_N3, topS, topC);
+    if (any) rare_sib<P>(st, smem, topS, topC);
 }
 
 // step_sib in pieces for the pipelined walk: the shared limb L (returns the
 // scaled carries into limb L + 1 of C and S) ...
 template <class P>
-__device__ __forceinline__ void sib_shared_step(State<P> &s0, u32 w1, u32 &cC, u32 &cS) {
+__device__ __forceinline__ void sib_shared_step(State<P> &s0, u32 w1, u32 &cC, u32 &cS, bool &wrap) {
     constexpr u32 ES = P::ES;
     constexpr int L = P::LO;
+    static_assert(L < P::ND && L < P::NN && P::FLAG_D1 == (1u << 30) && P::FLAG_N3 == (1u << 31),
+                  "sibling lanes: shared D1 / N3 limb and the low-digit entry's wrap flags");
     cC = __builtin_amdgcn_ubfe(w1, P::FC, P::FCW);
     {
         u32 t = P::TIGHT ? mad_u24<ES>(cC, s0.C[L]) : s0.C[L] + cC;
@@ -1325,6 +1367,13 @@ __device__ __forceinline__ void sib_shared_step(State<P> &s0, u32 w1, u32 &cC, u
         s0.S[L] = t - cS * P::B;
     }
     s0.r8 += ES;
+    // limb-0 wraps of D1 / N3 (the entry's flags, one in ~B / 5 steps) step
+    // their limb L here, without a branch; only limb L reaching B (one in
+    // ~B^2 / 5) takes the rare path.  (Branching on the flags sent a wave
+    // down the rare path on ~1 in 5 steps, mostly for this increment.)
+    s0.D1[L] += (w1 >> (30 - ilog2(ES))) & ES;
+    s0.N3[L] += (w1 >> (31 - ilog2(ES))) & ES;
+    wrap = (s0.D1[L] >= P::ESB) | (s0.N3[L] + (L < P::SL ? 3 * P::EBT : 0u) >= P::ESB);
 }
 
 // ... and one sibling's limbs above it (returns whether a top limb carried).
@@ -1434,7 +1483,12 @@ __device__ __forceinline__ void sib_count(const u32 (&m)[P::MW], int j, u32 i, c
         if (u > cutoff) {
             const SibUnit su = sib_unit<P>(a);
             u64 lo = su.lo, hi = su.hi;
-            add_u128(lo, hi, (u64)j * ((u64)P::B * P::B) + i);
+            // i opaque here: otherwise the compiler strength-reduces su.lo +
+            // j B^2 + i into three 64-bit induction variables stepped on
+            // every step of the walk for this once-in-1e8 branch
+            u32 ii = i;
+            asm volatile("" : "+v"(ii));
+            add_u128(lo, hi, (u64)j * ((u64)P::B * P::B) + ii);
             u32 pos = atomicAdd(out.count, 1u);
             if (pos < out.cap) {
                 out.n[2 * (u64)pos] = lo;
@@ -1475,12 +1529,12 @@ __device__ __forceinline__ void walk_sib_pipe(State<P> (&st)[P::SIB], const unsi
         // the shared limb's step (needs only the low-digit entry's carries)
         const u32 w1 = vlo.y;
         u32 cC, cS;
-        sib_shared_step<P>(st[0], w1, cC, cS);
+        bool any;
+        sib_shared_step<P>(st[0], w1, cC, cS, any);
         if (M > 1) sib_issue<P>(st[1], smem, e[1]);
         __builtin_amdgcn_sched_barrier(0);
         u32 m0[P::MW];
         bool topS[M], topC[M];
-        bool any = w1 >= P::FLAG_D1;
 #pragma unroll
         for (int j = 0; j < M; j++) {
             if (j == 0) {
@@ -1491,12 +1545,16 @@ __device__ __forceinline__ void walk_sib_pipe(State<P> (&st)[P::SIB], const unsi
 #pragma unroll
             for (int w = 0; w < P::MW; w++) m[w] = m0[w] | st[j].hi[w];
             sib_consume<P>(st[j], e[j], m);
-            sib_count<P>(m, j, i, smem, a, hbase, hinc, outl, cutoff, out);
+            // probe 16 (wrong by design): no window count, the mask feeds a
+            // register sum instead
+            if constexpr ((P::PROBE & 16) != 0) any |= (m[0] ^ m[1]) == 0x5a5a5a5au;
+            else sib_count<P>(m, j, i, smem, a, hbase, hinc, outl, cutoff, out);
             any |= sib_upper_step<P>(st[j], cC, cS, topS[j], topC[j]);
             if (j + 2 < M) sib_issue<P>(st[j + 2], smem, e[j + 2]);
             __builtin_amdgcn_sched_barrier(0);
         }
-        if (any) rare_sib<P>(st, smem, w1 & P::FLAG_D1, w1 & P::FLAG_N3, topS, topC);
+        // probe 8 (wrong by design): the rare path never runs
+        if ((P::PROBE & 8) == 0 && any) rare_sib<P>(st, smem, topS, topC);
     }
 }
 
@@ -1671,11 +1729,14 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
             State<P> sst[P::SIB];
             const SibUnit su = sib_unit<P>(a);
             if (su.active) {
+                u32 X[P::NX];
+                init_digits<P>(X, su.lo, su.hi);
+                init_plain<P>(sst[0], X);
+#pragma unroll
+                for (int j = 1; j < P::SIB; j++) sib_derive<P>(sst[j], sst[0], X, (u32)j);
 #pragma unroll
                 for (int j = 0; j < P::SIB; j++) {
-                    u64 lo = su.lo, hi = su.hi;
-                    add_u128(lo, hi, (u64)j * ((u64)P::B * P::B));
-                    init<P>(sst[j], lo, hi);
+                    init_scale<P>(sst[j]);
                     sib_park<P>(sst[j], j, smem);
                 }
             }

@@ -1,5 +1,5 @@
 """Per-base hardware bound of the FD detailed kernel from rocprofv3 --pmc passes
-of `bench.py --base B --mode detailed` (scripts/r04_measure.sh: gpurun_out/
+of `bench.py --base B --mode detailed` (scripts/r05_measure.sh: gpurun_out/
 pmc_b{B}_sq and pmc_b{B}_busy), 1e9 at each base's range start:
 
     python scripts/pmc_bases.py --out profiles/r04/pmc_bases.json gpurun_out 40 52 53 54 64 65 80

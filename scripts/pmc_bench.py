@@ -8,7 +8,14 @@ counter group per pass), for bench.py's roofline.frac_hw:
 Per-dispatch means over every fd2_kernel dispatch of every pass (warmup, timed
 region and the isolated launches alike: the kernel is the same launch each
 time).  Derived:
-  valu_busy           VALUBusy / 100 (SQ_ACTIVE_INST_VALU over GRBM_GUI_ACTIVE x CUs)
+  valu_busy           VALUBusy / 100 (SQ_ACTIVE_INST_VALU over GRBM_GUI_ACTIVE x CUs; the
+                      counter charges one cycle per instruction whatever its issue
+                      rate, so it is not an issue-slot share and can pass 1)
+  valu_issue_busy     the VALU issue-slot share: SQ_INSTS_VALU x (issue cycles per
+                      VALU instruction of the kernel's hot-loop mix, --valu-cpi, from
+                      scripts/isa/loop_budget.py on its ISA) / (4 SIMDs x CUs x
+                      kernel_cycles) -- reconciled: <= 1 by construction of the
+                      denominator, the SIMD cycles the kernel spans
   valu_lane_ops_per_n SQ_INSTS_VALU x 64 / numbers per dispatch
   lds_instr_per_n     SQ_INSTS_LDS x 64 / numbers
   lds_conflict_frac   SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
@@ -45,6 +52,9 @@ ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(os
                                            "nice_amd", "libnice_hip.so"))
 ap.add_argument("--cus", type=int, default=256)
 ap.add_argument("--xcds", type=int, default=8)
+ap.add_argument("--valu-cpi", type=float, default=None,
+                help="issue cycles per VALU instruction of the hot loop (ISA budget)")
+ap.add_argument("--valu-cpi-source", default=None, help="file the --valu-cpi figure comes from")
 ap.add_argument("dirs", nargs="+")
 a = ap.parse_args()
 
@@ -83,6 +93,10 @@ if "GRBM_GUI_ACTIVE" in mean:
     der["kernel_cycles"] = mean["GRBM_GUI_ACTIVE"] / a.xcds
     if "SQ_LDS_IDX_ACTIVE" in mean:
         der["lds_busy"] = mean["SQ_LDS_IDX_ACTIVE"] / a.cus / der["kernel_cycles"]
+    if "SQ_INSTS_VALU" in mean and a.valu_cpi:
+        der["valu_issue_busy"] = mean["SQ_INSTS_VALU"] * a.valu_cpi / (4 * a.cus * der["kernel_cycles"])
+        der["valu_cpi"] = a.valu_cpi
+        der["valu_cpi_source"] = a.valu_cpi_source
 if "SQ_LDS_IDX_ACTIVE" in mean and mean.get("SQ_INSTS_LDS"):
     der["lds_cycles_per_instr"] = mean["SQ_LDS_IDX_ACTIVE"] / mean["SQ_INSTS_LDS"]
 if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:

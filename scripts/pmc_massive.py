@@ -1,4 +1,4 @@
-"""msd_wave_kernel counters on the whole massive field (scripts/r04_measure.sh:
+"""msd_wave_kernel counters on the whole massive field (scripts/r05_measure.sh:
 rocprofv3 --pmc passes of scripts/massive_1gpu.py -> gpurun_out/pmc_massive_sq,
 pmc_massive_busy), with the field's totals from tests/golden/massive_b50.json and
 its one-GPU wall time from the configs run:

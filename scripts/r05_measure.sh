@@ -1,4 +1,4 @@
-# Round-4 measurement on one GPU (each step under its own limit via
+# Round-5 measurement on one GPU (each step under its own limit via
 # scripts/gpu.sh or timeout; stops at the first failure):
 #  - the default bench command under rocprofv3 (kernel trace + stats) and its
 #    --pmc passes (one counter group per pass) -> scripts/pmc_bench.py;
