@@ -12,10 +12,7 @@
 namespace nice {
 namespace fd2 {
 
-#ifdef NICE_PROBES
-u64 *g_stamps = nullptr;  // device buffer of the phase stamps (probe build)
-u64 g_last_launch[6] = {};
-#endif
+NICE_PROBE_ONLY(u64 *g_stamps = nullptr; u64 g_last_launch[6] = {};)  // phase stamps, last launch (probe build)
 
 // ---------------------------------------------------------------------------
 // Host: limb counts per segment.  For a segment [a, e) the last FD state a
@@ -114,45 +111,7 @@ static_assert(FD2_NPARTS == 6, "launch_part declarations");
 // no bignum work per launch).
 static hipError_t launch_segment(const DetailedLaunch &p, const Combo &c, int num_cus, hipStream_t s) {
     const int probe = (int)probe_knob("NICE_FD2_PROBE", 0);
-#ifdef NICE_PROBES
-    if (probe && p.base == 40 && c.nd == 4 && c.ne == 8 && c.ne2 == 5) {
-        if (probe == 1) return launch_cfg<Cfg<40, 4, 8, 5, 1>>(p, num_cus, s);
-        if (probe == 2) return launch_cfg<Cfg<40, 4, 8, 5, 2>>(p, num_cus, s);
-        if (probe == 3) return launch_cfg<Cfg<40, 4, 8, 5, 3>>(p, num_cus, s);
-        if (probe == 4) return launch_cfg<Cfg<40, 4, 8, 5, 4>>(p, num_cus, s);
-        // Workgroup-size sweep (profiles/r01/fd2_wg_sweep.log): 512 and 768
-        // (6 waves/SIMD) tie at 2.56-2.58 ms, 1024 (8 waves, spills) 2.59,
-        // 896 (7 waves) 2.85-2.92, 640 (5 waves) 3.18.
-        if (probe == 6) return launch_cfg<Cfg<40, 4, 8, 5, 0, 768>>(p, num_cus, s);
-        if (probe == 7) return launch_cfg<Cfg<40, 4, 8, 5, 0, 1024>>(p, num_cus, s);
-        if (probe == 5) return launch_cfg<Cfg<40, 4, 8, 5, 0, 896>>(p, num_cus, s);
-        if (probe == 8) return launch_cfg<Cfg<40, 4, 8, 5, 0, 512, 1>>(p, num_cus, s);
-        if (probe == 9) return launch_cfg<Cfg<40, 4, 8, 5, 0, 512, 17>>(p, num_cus, s);
-    }
-    // b80 VALU-decoded limbs (probe 30 + VD: 31..34 = 1..4 top C limbs, 47 =
-    // 1 C + 1 S, 48 = 2 C + 1 S), 1024-thread workgroups, main combo
-    if (probe >= 30 && p.base == 80 && c.nd == 8 && c.ne == 16 && c.ne2 == 9) {
-        if (probe == 31) return launch_cfg<Cfg<80, 8, 16, 9, 0, 1024, 1>>(p, num_cus, s);
-        if (probe == 32) return launch_cfg<Cfg<80, 8, 16, 9, 0, 1024, 2>>(p, num_cus, s);
-        if (probe == 33) return launch_cfg<Cfg<80, 8, 16, 9, 0, 1024, 3>>(p, num_cus, s);
-        if (probe == 34) return launch_cfg<Cfg<80, 8, 16, 9, 0, 1024, 4>>(p, num_cus, s);
-        if (probe == 36) return launch_cfg<Cfg<80, 8, 16, 9, 0, 1024, 6>>(p, num_cus, s);
-        if (probe == 47) return launch_cfg<Cfg<80, 8, 16, 9, 0, 1024, 17>>(p, num_cus, s);
-        if (probe == 48) return launch_cfg<Cfg<80, 8, 16, 9, 0, 1024, 18>>(p, num_cus, s);
-    }
-    if (probe >= 30 && p.base == 64 && c.nd == 7 && c.ne == 13 && c.ne2 == 7) {
-        if (probe == 31) return launch_cfg<Cfg<64, 7, 13, 7, 0, 512, 1>>(p, num_cus, s);
-        if (probe == 32) return launch_cfg<Cfg<64, 7, 13, 7, 0, 512, 2>>(p, num_cus, s);
-        if (probe == 33) return launch_cfg<Cfg<64, 7, 13, 7, 0, 512, 3>>(p, num_cus, s);
-        if (probe == 47) return launch_cfg<Cfg<64, 7, 13, 7, 0, 512, 17>>(p, num_cus, s);
-        if (probe == 48) return launch_cfg<Cfg<64, 7, 13, 7, 0, 512, 18>>(p, num_cus, s);
-    }
-    if (probe >= 30 && p.base == 68 && c.nd == 7 && c.ne == 14 && c.ne2 == 7) {
-        if (probe == 31) return launch_cfg<Cfg<68, 7, 14, 7, 0, 1024, 1>>(p, num_cus, s);
-        if (probe == 32) return launch_cfg<Cfg<68, 7, 14, 7, 0, 1024, 2>>(p, num_cus, s);
-        if (probe == 47) return launch_cfg<Cfg<68, 7, 14, 7, 0, 1024, 17>>(p, num_cus, s);
-    }
-#endif
+#include NICE_PROBE_INC("fd2_detailed_probe_dispatch.inc")
     // Fields too small to fill the chip keep 512-thread workgroups (the
     // per-workgroup table build dominates there: b80 1e6 kernel 30 vs 38 us);
     // probe 20 forces them for b80 comparisons.
@@ -194,7 +153,7 @@ hipError_t launch_detailed_fd2(const DetailedLaunch &p, int num_cus, hipStream_t
     const u128 e = a + p.count;
     DetailedLaunch q = p;
     // p.hist_copies: the same for every launch of the field (enqueue_detailed)
-    if (p.hist_copies < kHistCopies) q.hist_copies = (uint32_t)fd2::probe_knob("NICE_FD2_COPIES", p.hist_copies);
+    if (p.hist_copies < kHistCopies) q.hist_copies = (uint32_t)probe_knob("NICE_FD2_COPIES", p.hist_copies);
     if (q.hist_copies < 1 || q.hist_copies > kHistCopies) q.hist_copies = kHistCopies;
     for (size_t i = 0; i <= t.cuts.size() && a < e; i++) {
         u128 stop = i < t.cuts.size() && t.cuts[i] < e ? t.cuts[i] : e;
@@ -212,30 +171,4 @@ hipError_t launch_detailed_fd2(const DetailedLaunch &p, int num_cus, hipStream_t
 
 }  // namespace nice
 
-#ifdef NICE_PROBES
-// Probe build only: enable (1) the fd2 kernel's per-workgroup phase stamps
-// (kStampGroups x kStampWords words, zeroed), or read them into out[cap] and disable
-// (0).  Synchronous; for scripts/fd2_stamps.py.
-extern "C" int nice_probe_fd2_stamps(int enable, uint64_t *out, size_t cap) {
-    using nice::fd2::g_stamps;
-    const size_t words = (size_t)nice::fd2::kStampGroups * nice::fd2::kStampWords;
-    if (enable) {
-        if (!g_stamps && hipMalloc(&g_stamps, words * 8) != hipSuccess) return 2;
-        return hipMemset(g_stamps, 0, words * 8) == hipSuccess ? 0 : 2;
-    }
-    if (!g_stamps) return 1;
-    if (hipDeviceSynchronize() != hipSuccess) return 2;
-    const size_t n = cap < words ? cap : words;
-    if (out && n && hipMemcpy(out, g_stamps, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return 2;
-    (void)hipFree(g_stamps);
-    g_stamps = nullptr;
-    return 0;
-}
-
-// Probe build only: the launch geometry of the last fd2 launch (grid, WG,
-// chunk, nunits, tail, workgroups per CU).
-extern "C" int nice_probe_fd2_last(uint64_t *out6) {
-    for (int k = 0; k < 6; k++) out6[k] = nice::fd2::g_last_launch[k];
-    return 0;
-}
-#endif
+#include NICE_PROBE_INC("fd2_detailed_probe_exports.inc")

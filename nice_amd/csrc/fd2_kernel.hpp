@@ -58,6 +58,7 @@
 #include "host_math.hpp"
 #include "kernels.h"
 #include "nice_device.hpp"
+#include "probe.hpp"
 
 namespace nice {
 namespace fd2 {
@@ -76,14 +77,6 @@ constexpr bool split_exact(unsigned base, unsigned es, unsigned long long m) {
 // the probe build (make -C nice_amd probe -> libnice_hip_probe.so, used by
 // scripts/); the product library ignores the environment and always runs the
 // production configuration.
-#ifdef NICE_PROBES
-static u64 probe_knob(const char *name, u64 dflt) {
-    const char *v = getenv(name);
-    return v && *v ? strtoull(v, nullptr, 10) : dflt;
-}
-#else
-static constexpr u64 probe_knob(const char *, u64 dflt) { return dflt; }
-#endif
 
 // Histogram window [W0, W0 + W) per base: where the unique-count
 // distribution of in-range n lives (scripts/fd2_windows.py, 40 000 samples
@@ -965,38 +958,27 @@ static hipError_t fd2_tables(hipStream_t s, const uint4 **out) {
 // the caller's mapped result words and re-zeroes the state block, so a field
 // is ONE launch instead of main + tail + epilogue (under several fields in
 // flight each small launch waited for free CUs: 25-60 us apiece).
-#ifdef NICE_PROBES
 // Probe build: per-workgroup phase stamps (scripts/fd2_stamps.py).  When
 // g_stamps (host, set by nice_probe_fd2_stamps) is non-null, thread 0 of each
 // workgroup b < kStampGroups writes kStampWords words at stamps + kStampWords b:
 // for each phase k the constant 100 MHz real-time counter (word 2k) and the
 // shader clock (word 2k + 1).  The stamps go only to that buffer; nothing
 // reads them on the device.  Phases 7..9 are the finishing workgroup's
-// field finish.
+// field finish.  (Product build: kProbes is false and Fd2Args::stamps null, so
+// a stamp compiles to nothing.)
 constexpr u32 kStampGroups = 65536, kStampWords = 32;
-extern u64 *g_stamps;
-extern u64 g_last_launch[6];  // grid, WG, chunk, nunits, tail, per_cu of the last launch
+NICE_PROBE_ONLY(extern u64 *g_stamps; extern u64 g_last_launch[6];)  // last launch: grid, WG, chunk, nunits, tail, per_cu
 #define FD2_STAMP_P(p, k)                                                                        \
     do {                                                                                         \
-        if ((p) && threadIdx.x == 0 && blockIdx.x < kStampGroups) {                              \
+        if (kProbes && (p) && threadIdx.x == 0 && blockIdx.x < kStampGroups) {                   \
             (p)[kStampWords * (u64)blockIdx.x + 2 * (k)] = __builtin_amdgcn_s_memrealtime();     \
             (p)[kStampWords * (u64)blockIdx.x + 2 * (k) + 1] = __builtin_amdgcn_s_memtime();     \
         }                                                                                        \
     } while (0)
 #define FD2_STAMP(a, k) FD2_STAMP_P((a).stamps, k)
-#else
-#define FD2_STAMP_P(p, k) \
-    do {                  \
-    } while (0)
-#define FD2_STAMP(a, k) \
-    do {                \
-    } while (0)
-#endif
 
 struct Fd2Args {
-#ifdef NICE_PROBES
-    u64 *stamps;
-#endif
+    u64 *stamps;  // probe build: phase stamps (null in the product build)
     u64 start_lo, start_hi;
     u64 tail_lo, tail_hi;
     u32 nunits, chunk;
@@ -1314,10 +1296,12 @@ __device__ __forceinline__ void rare_sib(State<P> (&st)[P::SIB], const unsigned 
     }
 }
 
+template <class P>
+__device__ __forceinline__ void sib_shared_step(State<P> &s0, u32 w1, u32 &cC, u32 &cS, bool &wrap);
+
 // One FD step of all siblings (step() restated with the shared limb 1).
 template <class P>
 __device__ __forceinline__ void step_sib(State<P> (&st)[P::SIB], const unsigned char *smem, u32 w1) {
-    constexpr u32 ES = P::ES;
     constexpr int L = P::LO;
     constexpr int CT = P::CL - 1, ST = P::SL - 1;
     u32 cC, cS;
@@ -1825,11 +1809,7 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
     FD2_STAMP(a, 5);  // histogram flushed (thread 0's part)
     if (a.fin.out_mapped) {
         __syncthreads();  // smem is reused by the finish
-#ifdef NICE_PROBES
         field_finish<P::WG>(a.fin, a.hist, a.ncopies, out.count, smem, a.stamps);
-#else
-        field_finish<P::WG>(a.fin, a.hist, a.ncopies, out.count, smem, nullptr);
-#endif
     }
     FD2_STAMP(a, 6);  // end (the finishing workgroup: after the finish)
 }
@@ -2050,9 +2030,7 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         }
         const u64 main_blocks = (nunits + P::WG - 1) / P::WG;  // one chunk per lane
         Fd2Args a{};
-#ifdef NICE_PROBES
-        a.stamps = g_stamps;
-#endif
+        NICE_PROBE_ONLY(a.stamps = g_stamps;)
         a.start_lo = q.start_lo;
         a.start_hi = q.start_hi;
         a.tail_lo = q.start_lo;
@@ -2070,12 +2048,10 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         a.tabs = tabs;
         // the field's finish rides on its last launch
         a.fin = left == cnt ? q.fin : FieldFinish{nullptr, nullptr};
-#ifdef NICE_PROBES
-        {
+        NICE_PROBE_ONLY({
             const u64 v[6] = {grid, (u64)P::WG, chunk, nunits, tail, (u64)per_cu};
             for (int k = 0; k < 6; k++) g_last_launch[k] = v[k];
-        }
-#endif
+        })
         hipLaunchKernelGGL(kern, dim3((u32)grid), dim3(P::WG), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (p.launches) ++*p.launches;
@@ -2153,9 +2129,7 @@ static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s
             tail = R - nunits * chunk;
         }
         Fd2Args a{};
-#ifdef NICE_PROBES
-        a.stamps = g_stamps;
-#endif
+        NICE_PROBE_ONLY(a.stamps = g_stamps;)
         a.sib_lo = q.start_lo;
         a.sib_hi = q.start_hi;
         a.sib_chunk = (u32)L;
@@ -2186,12 +2160,10 @@ static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s
         a.tabs = tabs;
         a.fin = left == cnt ? q.fin : FieldFinish{nullptr, nullptr};
         const u64 grid = (u64)a.sib_blocks + a.edge_blocks + a.main_blocks + (tail + P::WG - 1) / P::WG;
-#ifdef NICE_PROBES
-        {
+        NICE_PROBE_ONLY({
             const u64 v[6] = {grid, (u64)P::WG, L, Q * upb, R, (u64)per_cu};
             for (int k = 0; k < 6; k++) g_last_launch[k] = v[k];
-        }
-#endif
+        })
         hipLaunchKernelGGL(kern, dim3((u32)grid), dim3(P::WG), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (p.launches) ++*p.launches;

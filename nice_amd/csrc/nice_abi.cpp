@@ -32,6 +32,7 @@
 #include "../../include/nice_hip.h"
 #include "host_math.hpp"
 #include "kernels.h"
+#include "probe.hpp"
 #include "radix_fast.hpp"
 
 using nice::u128;
@@ -56,33 +57,18 @@ thread_local std::string g_err;
 // by polling the sequence word it publishes in mapped memory (default), or
 // (probe build: NICE_SPIN=0) by the stream's completion event.
 inline bool spin_wait() {
-#ifdef NICE_PROBES
-    static const bool v = !getenv("NICE_SPIN") || atoi(getenv("NICE_SPIN")) != 0;
-    return v;
-#else
-    return true;
-#endif
+    return nice::probe_knob("NICE_SPIN", 1) != 0;
 }
 
 // Streams of a device's slots: bit 0 = the slots share ONE detailed stream
 // (consecutive detailed fields run back to back instead of overlapping at
 // their edges), bit 1 = they share one niceonly stream.
 inline int shared_streams() {
-#ifdef NICE_PROBES
-    static const int v = getenv("NICE_SHARED_STREAMS") ? atoi(getenv("NICE_SHARED_STREAMS")) : 0;
-    return v;
-#else
-    return 0;
-#endif
+    return (int)nice::probe_knob("NICE_SHARED_STREAMS", 0);
 }
 
 inline int slots_used() {
-#ifdef NICE_PROBES
-    static const int n = getenv("NICE_SLOTS") ? std::max(1, std::min(kSlots, atoi(getenv("NICE_SLOTS")))) : kSlots;
-    return n;
-#else
-    return kSlots;
-#endif
+    return std::max(1, std::min(kSlots, (int)nice::probe_knob("NICE_SLOTS", kSlots)));
 }
 
 int fail(int code, const std::string &msg) {
@@ -355,9 +341,7 @@ int slot_init(Device &d, Slot &sl, const Slot *share) {
     }
     int least = 0, greatest = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-#ifdef NICE_PROBES
-    if (getenv("NICE_NICE_PRIO") && atoi(getenv("NICE_NICE_PRIO")) == 0) greatest = least;
-#endif
+    if (nice::probe_set("NICE_NICE_PRIO") && nice::probe_knob("NICE_NICE_PRIO", 1) == 0) greatest = least;
     if (share && (shared_streams() & 2)) {
         sl.nstream = share->nstream;
     } else {
@@ -522,9 +506,7 @@ int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *f
             const bool last = a + c == e;
             p.fin = last && fd ? nice::FieldFinish{sl.d_fin, sl.d_done, sl.seq}
                                : nice::FieldFinish{nullptr, nullptr, 0};
-#ifdef NICE_PROBES
-            if (getenv("NICE_FD2_NOFIN")) p.fin = nice::FieldFinish{nullptr, nullptr, 0};  // probe: finish kernel
-#endif
+            if (nice::probe_set("NICE_FD2_NOFIN")) p.fin = nice::FieldFinish{nullptr, nullptr, 0};  // probe: finish kernel
             const bool fd2 = fd;
             hipError_t err = fd ? nice::launch_detailed_fd2(p, d.num_cus, sl.stream)
                                 : nice::launch_detailed_generic(p, d.num_cus, sl.stream);
@@ -1402,9 +1384,7 @@ int niceonly_enqueue(nice_ctx *ctx, int t, NiceJob &job) {
         // at 164, 0.17 s at 328 (profiles/r02/massive_batch_sweep.log).
         const uint64_t fl = std::min<uint64_t>(floor_size, 1ull << 30);
         uint64_t cpb = std::max<uint64_t>(1, (fl << 27) / cnk);
-#ifdef NICE_PROBES
-        if (getenv("NICE_MSD_CPB")) cpb = std::max<uint64_t>(1, strtoull(getenv("NICE_MSD_CPB"), nullptr, 10));
-#endif
+        if (nice::probe_set("NICE_MSD_CPB")) cpb = std::max<uint64_t>(1, nice::probe_knob("NICE_MSD_CPB", 1));
         cpb = std::min(cpb, mine);
         const uint64_t batch_n = cpb * cnk;
         uint64_t per = std::min<uint64_t>(batch_n / fl + cpb, cpb << 22) + 64;
@@ -1413,12 +1393,9 @@ int niceonly_enqueue(nice_ctx *ctx, int t, NiceJob &job) {
         const uint64_t leaf_cap = std::min<uint64_t>(per + (batch_n / nice::kLeafPiece) + 64, 0xffffffffull);
         // Chunks whose recursion fits a workgroup run fused: one launch per
         // batch, one workgroup per chunk (grid-strided), no level queues.
-#ifdef NICE_PROBES
-        const uint32_t fcap = getenv("NICE_MSD_FCAP") && cnk <= 0xffffffffull
-                                  ? (uint32_t)atoi(getenv("NICE_MSD_FCAP")) : nice::msd_fused_cap(cnk, floor_size);
-#else
-        const uint32_t fcap = nice::msd_fused_cap(cnk, floor_size);
-#endif
+        const uint32_t fcap = nice::probe_set("NICE_MSD_FCAP") && cnk <= 0xffffffffull
+                                  ? (uint32_t)nice::probe_knob("NICE_MSD_FCAP", 0)
+                                  : nice::msd_fused_cap(cnk, floor_size);
         // Chunks too large for the fused kernel: the level BFS only down to a
         // root level `wlevel` (nodes <= 2^26 numbers, ~2048 roots per wave of
         // the fused MSD + candidate kernel), then msd_wave_kernel.  Nothing of
@@ -1427,9 +1404,7 @@ int niceonly_enqueue(nice_ctx *ctx, int t, NiceJob &job) {
         // queues: 2^24 nodes at the root level.  The massive field is ONE
         // batch.
         bool wave = !fcap;
-#ifdef NICE_PROBES
-        if (getenv("NICE_MSD_NOWAVE")) wave = false;  // A/B: the level-BFS + leaf-list path
-#endif
+        if (nice::probe_set("NICE_MSD_NOWAVE")) wave = false;  // A/B: the level-BFS + leaf-list path
         uint32_t wlevel = 0, wgrid = 0;
         uint64_t wleaf_cap = 0;
         if (wave) {
@@ -1440,9 +1415,7 @@ int niceonly_enqueue(nice_ctx *ctx, int t, NiceJob &job) {
             // at 2048; a 1/8 dealt share 0.0135 / 0.0101 s, scripts/roots_sweep.py)
             const uint64_t waves = (uint64_t)wgrid * nice::msd_wave_waves_per_group();
             uint64_t target = waves * 2048;
-#ifdef NICE_PROBES
-            if (getenv("NICE_MSD_ROOTS")) target = waves * strtoull(getenv("NICE_MSD_ROOTS"), nullptr, 10);
-#endif
+            if (nice::probe_set("NICE_MSD_ROOTS")) target = waves * nice::probe_knob("NICE_MSD_ROOTS", 1);
             uint32_t last = 0;  // first level without splits
             while (last < 22 && ((cnk + (1ull << last) - 1) >> last) >= 2 * fl) last++;
             while (wlevel < last && ((cnk + (1ull << wlevel) - 1) >> wlevel) > (1ull << 26)) wlevel++;
@@ -1509,9 +1482,7 @@ int niceonly_enqueue(nice_ctx *ctx, int t, NiceJob &job) {
             mp.M = (uint32_t)M;
             mp.base = base;
             mp.in_range = in_range;
-#ifdef NICE_PROBES
-            mp.probe = getenv("NICE_MSD_PROBE") ? (uint32_t)atoi(getenv("NICE_MSD_PROBE")) : 0u;
-#endif
+            mp.probe = (uint32_t)nice::probe_knob("NICE_MSD_PROBE", 0);
             nice::NiceonlyLaunch p{};
             if (wave) {
                 p.residues = mp.residues;
@@ -1720,13 +1691,11 @@ int niceonly_gather(nice_ctx *ctx, NiceJob &job, int t, std::vector<uint32_t> &c
         if (job.on_device) {
             const uint32_t *c = sl.h_msd;
             sl.msd.dirty = false;  // the epilogue re-zeroed counters and count
-#ifdef NICE_PROBES
-            if (getenv("NICE_MSD_TRACE")) {  // level sizes of the last batch (diagnostics)
+            if (nice::probe_set("NICE_MSD_TRACE")) {  // level sizes of the last batch (diagnostics)
                 fprintf(stderr, "msd levels:");
                 for (int lv = 0; lv < 24; lv++) fprintf(stderr, " %u", c[lv]);
                 fprintf(stderr, " | ranges %u\n", c[26]);
             }
-#endif
             if (c[25])
                 return fail(NICE_ERR_MSD_OVERFLOW, "device MSD queue overflow (msd_floor too small "
                                                "for chunk_size); use msd_where = host");

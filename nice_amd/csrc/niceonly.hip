@@ -25,6 +25,7 @@
 // finds in the same launch (see there).
 #include "kernels.h"
 #include "nice_device.hpp"
+#include "probe.hpp"
 #include "radix_fast.hpp"
 
 namespace nice {
@@ -506,11 +507,7 @@ __device__ __forceinline__ u32 classify_node(const MsdLaunch &p, u32 level, u64 
     if (leaf) return 1;
     u64 l_lo = lo, l_hi = hi;
     add_u128(l_lo, l_hi, size - 1);
-#ifdef NICE_PROBES
-    const bool no_skip_test = p.probe & 1;
-#else
-    constexpr bool no_skip_test = false;
-#endif
+    const bool no_skip_test = kProbes && (p.probe & 1);
     bool skip = false;
     if (size != 1 && !no_skip_test) {
         if constexpr (IsConst<G>::value) {
@@ -532,11 +529,9 @@ template <u32 MC>
 __device__ __forceinline__ void append_leaf(const MsdLaunch &p, u32 act, u64 lo, u64 hi, u64 size,
                                             u32 *slots, u64 &n_st, u64 &c_st, u64 &s_st) {
     LeafDesc ld{0, 0, 0, 0};
-#ifdef NICE_PROBES
-    if (act == 1 && (p.probe & 2)) {
+    if (kProbes && act == 1 && (p.probe & 2)) {
         ld = LeafDesc{lo, hi, size, 0};
     } else
-#endif
     if (act == 1) {
         ld = leaf_desc<MC>(lo, hi, size, p);
     }
@@ -872,11 +867,7 @@ msd_wave_kernel(MsdLaunch p, NiceonlyLaunch c, u32 level0, StackNode *scratch, G
             c_st += ld.count;
             s_st += nd.size;
         }
-#ifdef NICE_PROBES
-        const bool put = act == 1 && ld.count != 0 && !(p.probe & 4);  // probe 4: MSD only
-#else
-        const bool put = act == 1 && ld.count != 0;
-#endif
+        const bool put = act == 1 && ld.count != 0 && !(kProbes && (p.probe & 4));  // probe 4: MSD only
         const u64 bl = __ballot(put);
         if (put) {
             if constexpr (WALK) qw[(lq_tail + lane_rank(bl)) & (kWalkQ - 1)] = LeafW{ld.b0_lo, ld.g0, (u32)ld.count};
