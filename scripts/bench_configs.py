@@ -24,6 +24,9 @@ import nice_amd as N  # noqa: E402
 from nice_amd.benchmark import BenchmarkMode as BM, get_benchmark_field  # noqa: E402
 
 
+THROUGHPUT_FLOOR = 64
+
+
 def timed(fn, reps):
     fn()
     ts = []
@@ -126,6 +129,33 @@ def main():
                 "note": f"each of {W} ranks' dealt share of the whole field timed alone on one GPU; "
                         f"numbers_per_sec = field / slowest share (the {W}-GPU field time without "
                         f"the exchange)"})
+    # The same field at the throughput floor: MSD recursion down to nodes of
+    # <= 2 * 64 numbers (depth 20 of its 1e8 chunks) instead of < 500 (depth
+    # 18), trading 7.5e9 stride candidates for 1.9e9 and deeper recursion
+    # (scripts/massive_floor_sweep.py: the fastest floor on one GPU,
+    # profiles/r05/massive_floor_low.log).  The nice list is floor-independent
+    # and must equal the fixture's; ranges / candidates are this floor's own.
+    sec, (lst, st) = timed(lambda: ctx.niceonly_raw(m.range_start, m.range_end, 50, chunk_size=10 ** 8,
+                                                     msd_floor=THROUGHPUT_FLOOR, msd_where="device"), 3)
+    assert [str(x) for x in lst] == [str(x) for w in fx["windows"] for x in w["nice_numbers"]], lst
+    out.append({"config": f"massive-floor-{THROUGHPUT_FLOOR}", "mode": "niceonly", "base": 50,
+                "size": m.range_size, "numbers_per_sec": m.range_size / sec, "wall_ms": sec * 1e3,
+                "msd_floor": THROUGHPUT_FLOOR, "msd_ranges": st.ranges, "candidates": st.candidates,
+                "nice": [str(x) for x in lst], "chunk": 10 ** 8,
+                "note": "whole field, throughput MSD floor (parity row: 'massive', floor 250)"})
+    t1f = sec * 1e3
+    shares = []
+    for r in range(W):
+        sec, (lst, st) = timed(lambda: ctx.niceonly_raw(m.range_start, m.range_end, 50, chunk_size=10 ** 8,
+                                                         msd_floor=THROUGHPUT_FLOOR, msd_where="device",
+                                                         deal_stride=W, deal_offset=r), 3)
+        shares.append({"rank": r, "wall_ms": sec * 1e3, "candidates": st.candidates, "msd_ranges": st.ranges,
+                       "nice": len(lst)})
+    tmax = max(x["wall_ms"] for x in shares)
+    out.append({"config": f"massive-floor-{THROUGHPUT_FLOOR}-dealt-{W}", "mode": "niceonly", "base": 50,
+                "size": m.range_size, "world": W, "msd_floor": THROUGHPUT_FLOOR, "max_share_wall_ms": tmax,
+                "t1_wall_ms": t1f, "numbers_per_sec": m.range_size / (tmax / 1e3),
+                "projected_efficiency": t1f / (W * tmax), "shares": shares})
     nice("msd-effective", get_benchmark_field(BM.MSD_EFFECTIVE), reps=3)
     nice("msd-ineffective", get_benchmark_field(BM.MSD_INEFFECTIVE))
     for r in out:

@@ -1,6 +1,7 @@
 """Whole massive benchmark field (b50, [start, start + 1e13), niceonly, client
-chunking 1e8, device MSD floor 250) on one GPU: wall time, MSD leaves,
-candidates, nice list.  Progress: one line per 1e12 slice."""
+chunking 1e8, device MSD floor 250 or argv[2]) on one GPU: wall time, MSD
+leaves, candidates, nice list.  Progress: one line per 1e12 slice.
+    python scripts/massive_1gpu.py [slices=10] [floor=250]"""
 import json
 import os
 import sys
@@ -14,6 +15,7 @@ from nice_amd.benchmark import BenchmarkMode as BM, get_benchmark_field  # noqa:
 f = get_benchmark_field(BM.MASSIVE)
 ctx = N.GpuContext(0)
 slices = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+floor = int(sys.argv[2]) if len(sys.argv) > 2 else 250
 step = f.range_size // slices
 tot = {"ranges": 0, "candidates": 0, "range_numbers": 0, "nice": []}
 t0 = time.perf_counter()
@@ -21,7 +23,7 @@ for i in range(slices):
     a = f.range_start + i * step
     b = f.range_end if i == slices - 1 else a + step
     t = time.perf_counter()
-    lst, st = ctx.niceonly_raw(a, b, 50, chunk_size=10 ** 8)
+    lst, st = ctx.niceonly_raw(a, b, 50, chunk_size=10 ** 8, msd_floor=floor, msd_where="device")
     tot["ranges"] += st.ranges
     tot["candidates"] += st.candidates
     tot["range_numbers"] += st.range_numbers

@@ -18,6 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ap = argparse.ArgumentParser()
 ap.add_argument("--out", required=True)
 ap.add_argument("--configs", required=True)
+ap.add_argument("--floor", type=int, default=250, help="the MSD floor the passes ran at")
 ap.add_argument("--cus", type=int, default=256)
 ap.add_argument("--xcds", type=int, default=8)
 ap.add_argument("--lib", default=os.path.join(ROOT, "nice_amd", "libnice_hip.so"))
@@ -36,10 +37,17 @@ for d in a.dirs:
         for (_, c), v in per.items():
             vals[c].append(v)
 m = {c: sum(v) / len(v) for c, v in vals.items()}
-fx = json.load(open(os.path.join(ROOT, "tests", "golden", "massive_b50.json")))
-cand = sum(w["candidates"] for w in fx["windows"])
-ranges = sum(w["ranges"] for w in fx["windows"])
-wall = [json.loads(l) for l in open(a.configs) if '"config": "massive"' in l][0]["wall_ms"]
+# floor 250: the field's totals from the oracle's fixture; other floors: the
+# configs run's own row at that floor (massive-floor-F)
+name = "massive" if a.floor == 250 else f"massive-floor-{a.floor}"
+row = [json.loads(l) for l in open(a.configs) if json.loads(l)["config"] == name][0]
+if a.floor == 250:
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "massive_b50.json")))
+    cand = sum(w["candidates"] for w in fx["windows"])
+    ranges = sum(w["ranges"] for w in fx["windows"])
+else:
+    cand, ranges = row["candidates"], row["msd_ranges"]
+wall = row["wall_ms"]
 cyc = m["GRBM_GUI_ACTIVE"] / a.xcds
 with open(a.lib, "rb") as fh:
     sha16 = hashlib.sha256(fh.read()).hexdigest()[:16]
@@ -50,7 +58,7 @@ der = {"kernel_cycles": cyc, "kernel_ms_at_2_4GHz": cyc / 2.4e6, "valu_busy": m[
        "lds_instr_per_candidate": m["SQ_INSTS_LDS"] * 64 / cand,
        "whole_field_wall_ms": wall, "candidates_per_sec_whole_field_wall": cand / (wall / 1e3)}
 out = {"kernel": sorted(names)[0] if names else None,
-       "field": "massive b50 [start, +1e13), client chunk 1e8, floor 250, device MSD",
+       "field": f"massive b50 [start, +1e13), client chunk 1e8, floor {a.floor}, device MSD",
        "lib_sha16": sha16, "candidates": cand, "msd_ranges": ranges,
        "per_dispatch": {c: round(v, 4) for c, v in sorted(m.items())}, "derived": der, "files": files,
        "note": "one dispatch of msd_wave_kernel runs the whole field's MSD recursion below the BFS root "
