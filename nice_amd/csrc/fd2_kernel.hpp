@@ -2081,10 +2081,15 @@ static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s
     if (per_cu_q < 0) return hipErrorInvalidDeviceFunction;
     const int per_cu = per_cu_q < 1 ? 1 : per_cu_q;
     constexpr u64 D = (u64)P::B * P::B, SB = (u64)P::SIB * D;
-    // too short for the sibling walk to pay: the same base without siblings
-    if (p.count < 4 * SB) return launch_cfg<typename P::NoSib>(p, num_cus, s);
-    if (p.cutoff + 1 < (u32)(P::W0 + P::W)) return hipErrorInvalidValue;
     const u64 lanes = (u64)num_cus * per_cu * P::WG;
+    // Too short for the sibling walk to pay: the same base without siblings.
+    // Below ~3 rounds of the resident lanes' units (b40: ~1.9e8 numbers) the
+    // 4-wave sibling grid's last round and its init outweigh the shared
+    // limbs: 1e8 0.274 vs 0.241 ms, 2e8 0.444 vs 0.438, 3e8 0.590 vs 0.708
+    // (profiles/r05/sib_threshold.log).
+    if (p.count < 4 * SB || p.count < 3 * lanes * P::SIB * P::TCHUNK)
+        return launch_cfg<typename P::NoSib>(p, num_cus, s);
+    if (p.cutoff + 1 < (u32)(P::W0 + P::W)) return hipErrorInvalidValue;
     const uint4 *tabs = nullptr;
     hipError_t e = fd2_tables<P>(s, &tabs);
     if (e != hipSuccess) return e;

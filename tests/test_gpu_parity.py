@@ -1261,18 +1261,18 @@ def test_eight_shard_context():
 
 @pytest.mark.parametrize("frac", [0.0, 0.1, 0.2926, 0.45, 0.97])
 def test_sibling_kernel_equals_small_fields(ctx, frac):
-    """b40 fields of >= 1e7 (and >= 4 super-blocks of 3 x 40^4 numbers) run
-    the sibling-lane kernel (Cfg::SIB = 3, fd2_kernel.hpp: a lane steps n,
-    n + B^2 and n + 2 B^2 together, sharing limbs 0 and 1; super-blocks,
-    edge units where the lane stride does not divide B^2, and the regular
-    remainder in one launch; the lane stride from the bank-conflict model).
-    Fields below 1e7 run the round-4 kernel at 512 threads.  A field of
-    ragged size at several points of the range (0.2926: across the limb-count
-    cut at 2n + 1 = 40^8) must equal the sum of its sub-1e7 pieces, and every
-    near-miss must recompute by the oracle."""
+    """b40 fields of >= ~1.9e8 numbers (3 rounds of the resident lanes' units,
+    launch_sib) run the sibling-lane kernel (Cfg::SIB = 3, fd2_kernel.hpp: a
+    lane steps n, n + B^2 and n + 2 B^2 together, sharing limbs 0 and 1;
+    super-blocks, edge units where the lane stride does not divide B^2, and
+    the regular remainder in one launch; the lane stride from the
+    bank-conflict model).  Shorter fields run the round-4 kernel (512 threads
+    below 1e7).  A field of ragged size at several points of the range
+    (0.2926: across the limb-count cut at 2n + 1 = 40^8) must equal the sum of
+    its sub-1e7 pieces, and every near-miss must recompute by the oracle."""
     r0, r1 = O.base_range(40)
     s = r0 + int((r1 - r0) * frac) + 12345
-    n = 4 * 3 * 1600 ** 2 + 2_345_677  # 4 super-blocks + a remainder
+    n = 26 * 3 * 1600 ** 2 + 2_345_677  # 26 super-blocks (2.0e8) + a remainder
     if s + n > r1:
         s = r1 - n
     h, l = ctx.detailed_raw(s, s + n, 40)
