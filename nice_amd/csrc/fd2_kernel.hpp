@@ -1859,15 +1859,17 @@ static const std::vector<float> &progression_cost(int slots) {
         double sum = 0;
         for (int ai = 0; ai < 16; ai++) {
             const double a = ai / 16.0 + 0.03125;
-            int cnt[32] = {}, seen[32][32];
+            // the lane values floor(a + d l) never decrease with l, so a
+            // value repeats only in consecutive lanes (a broadcast)
+            int cnt[32] = {};
             int best = 0;
+            long prev = -1;
             for (int l = 0; l < slots; l++) {
-                const long v = (long)std::floor(a + d * l) + 1000000L * slots;  // >= 0
-                const int sl = (int)(v % slots);
-                bool dup = false;
-                for (int q = 0; q < cnt[sl]; q++) dup |= seen[sl][q] == (int)(v % 100000);
-                if (!dup) seen[sl][cnt[sl]++] = (int)(v % 100000);
-                best = std::max(best, cnt[sl]);
+                const long v = (long)(a + d * l);  // a + d l >= 0: truncation is floor
+                if (v == prev) continue;
+                prev = v;
+                const int sl = (int)(v & (slots - 1));  // slots: 16 or 32
+                best = std::max(best, ++cnt[sl]);
             }
             sum += best;
         }
@@ -1881,46 +1883,65 @@ static const std::vector<float> &progression_cost(int slots) {
 // first_limb on, where the lanes' quadratic drift stays under half a unit)
 // at lane stride L, averaged over the segment's start, middle and end.  The
 // other limbs' values are effectively random whatever L is and are left out.
+// Per limb and point the lane step is c L and the drift k L^2 (c = f'(n) /
+// B^q, k = f''(n) 64^2 / 2 / B^q), so the strides of one pick share them.
 template <class P>
-static double lookup_conflict_model(long double n0, long double span, u64 L, int first_limb) {
-    constexpr int SLOTS = P::ES == 16 ? 16 : 32;
-    constexpr int NPASS = 64 / SLOTS;
-    const std::vector<float> &tab = progression_cost(SLOTS);
-    double cost = 0;
-    for (int pt = 0; pt < 3; pt++) {
-        const long double n = n0 + span * (long double)pt / 2;
-        const long double w = (long double)L * 64;  // the wave's span of n
-        for (int cube = 0; cube < 2; cube++) {
-            const int hi = cube ? P::CL : P::SL;
-            long double bq = 1;
-            for (int q = 0; q < first_limb; q++) bq *= (long double)P::B;
-            for (int q = first_limb; q < hi; q++, bq *= (long double)P::B) {
-                if (cube ? P::vd_c(q) : P::vd_s(q)) continue;
-                const long double f1 = cube ? 3 * n * n : 2 * n;   // f'(n)
-                const long double f2 = cube ? 6 * n : 2;           // f''(n)
-                if (f2 * w * w / 2 / bq >= 0.5L) continue;         // drifting: effectively random
-                const long double d = f1 * (long double)L / bq;    // lane step in limb units
-                const long double r = d < SLOTS ? d : SLOTS + fmodl(d, (long double)SLOTS);
-                cost += NPASS * tab[std::min<size_t>(tab.size() - 1, (size_t)(r * 64))];
+struct ConflictModel {
+    static constexpr int SLOTS = P::ES == 16 ? 16 : 32;
+    static constexpr int NPASS = 64 / SLOTS;
+    int n = 0;
+    double c[3 * (P::SL + P::CL)], k[3 * (P::SL + P::CL)];
+    const std::vector<float> *tab;
+    ConflictModel(long double n0, long double span, int first_limb) : tab(&progression_cost(SLOTS)) {
+        for (int pt = 0; pt < 3; pt++) {
+            const long double x = n0 + span * (long double)pt / 2;
+            for (int cube = 0; cube < 2; cube++) {
+                const int hi = cube ? P::CL : P::SL;
+                long double bq = 1;
+                for (int q = 0; q < first_limb; q++) bq *= (long double)P::B;
+                for (int q = first_limb; q < hi; q++, bq *= (long double)P::B) {
+                    if (cube ? P::vd_c(q) : P::vd_s(q)) continue;
+                    const long double f1 = cube ? 3 * x * x : 2 * x;  // f'(n)
+                    const long double f2 = cube ? 6 * x : 2;          // f''(n)
+                    c[n] = (double)(f1 / bq);
+                    k[n] = (double)(f2 * 4096 / 2 / bq);
+                    n++;
+                }
             }
         }
     }
-    return cost / 3;
-}
+    double cost(u64 L) const {
+        double sum = 0;
+        const double l = (double)L;
+        for (int i = 0; i < n; i++) {
+            if (k[i] * l * l >= 0.5) continue;  // drifting: effectively random
+            // the lane step in limb units: < 2^24 for every limb that passes
+            // the drift test, so double keeps its fraction
+            const double d = c[i] * l;
+            const double r = d < SLOTS ? d : SLOTS + (d - SLOTS * std::floor(d / SLOTS));
+            sum += NPASS * (*tab)[std::min<size_t>(tab->size() - 1, (size_t)(r * 64))];
+        }
+        return sum / 3;
+    }
+};
 
 // The odd stride in [lo, hi] with the lowest modelled cost at the segment
 // [start, start + count); among the strides within `tol` modelled cycles of
 // the best, the one closest to target (a lane's init amortises over its
 // chunk).  A few hundred table lookups: cheap enough for every launch.
+// (A rounds-aware pick -- the stride whose units fill whole rounds of the
+// resident lanes, times L plus init steps -- chose L ~ 130-160 and lost on
+// small fields: b40 1e8 0.261 ms against 0.227 at L = 65, and did not gain at
+// 1e9; profiles/r05/picker_rounds.log.)
 template <class P>
 static u64 pick_lane_stride(u128 start, u64 count, u64 lo, u64 hi, u64 target, int first_limb,
                             double tol = 0.5) {
-    const long double n0 = (long double)start;
+    const ConflictModel<P> m((long double)start, (long double)count, first_limb);
     double cost[512];
     int nc = 0;
     double min_cost = 1e30;
     for (u64 L = lo | 1; L <= hi && nc < 512; L += 2, nc++) {
-        cost[nc] = lookup_conflict_model<P>(n0, (long double)count, L, first_limb);
+        cost[nc] = m.cost(L);
         min_cost = std::min(min_cost, cost[nc]);
     }
     u64 best = target | 1, best_d = ~0ull;
@@ -2083,11 +2104,16 @@ static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s
     constexpr u64 D = (u64)P::B * P::B, SB = (u64)P::SIB * D;
     const u64 lanes = (u64)num_cus * per_cu * P::WG;
     // Too short for the sibling walk to pay: the same base without siblings.
-    // Below ~3 rounds of the resident lanes' units (b40: ~1.9e8 numbers) the
-    // 4-wave sibling grid's last round and its init outweigh the shared
-    // limbs: 1e8 0.274 vs 0.241 ms, 2e8 0.444 vs 0.438, 3e8 0.590 vs 0.708
-    // (profiles/r05/sib_threshold.log).
-    if (p.count < 4 * SB || p.count < 3 * lanes * P::SIB * P::TCHUNK)
+    // Fewer than 3 rounds of the resident lanes' units (at the target
+    // stride; decided before the stride pick, whose ~20 us of host work
+    // would otherwise delay the fallback's launch): the part-filled last
+    // round of the 4-wave grid and the stride's luck decide (b40 1e8: 0.227
+    // ms at L = 65, 1.95 rounds; 0.266 at L = 81, 1.57; the regular kernel
+    // 0.244; at 1e8-1.25e8 the two kernels trade +-6 %, from 2.5e8 the
+    // sibling kernel wins by 6-17 %: profiles/r05/sib_small_l.log,
+    // picker_rounds.log, sib_threshold.log, sib_final_thr.log).
+    if (p.count < 4 * SB ||
+        10 * (p.count / SB) * (D / P::TCHUNK) < (u64)probe_knob("NICE_FD2_SIBROUNDS", 30) * lanes)
         return launch_cfg<typename P::NoSib>(p, num_cus, s);
     if (p.cutoff + 1 < (u32)(P::W0 + P::W)) return hipErrorInvalidValue;
     const uint4 *tabs = nullptr;

@@ -284,7 +284,7 @@ def test_product_library_has_no_probe_kernels():
         blob = f.read()
     for knob in (b"NICE_FD2_PROBE", b"NICE_MSD_PROBE", b"NICE_FD_VARIANT", b"NICE_FD2_TCHUNK",
                  b"NICE_FD2_MINCHUNK", b"NICE_FD2_WG512", b"NICE_MSD_TRACE", b"NICE_FD2_LG",
-                 b"NICE_FD2_COPIES", b"NICE_FD2_VD", b"NICE_FD2_PERS", b"NICE_FD2_SIB",
+                 b"NICE_FD2_COPIES", b"NICE_FD2_VD", b"NICE_FD2_PERS", b"NICE_FD2_SIB", b"NICE_FD2_SIBROUNDS",
                  b"NICE_FD2_NOMODEL"):
         assert knob not in blob, knob
 
