@@ -1956,6 +1956,41 @@ static u64 pick_lane_stride(u128 start, u64 count, u64 lo, u64 hi, u64 target, i
     return best;
 }
 
+// The stride for fields of a few rounds (fewer than 3 at the target
+// stride): among the odd L in [lo, hi] the model does not flag, the one
+// whose units fill the fewest whole rounds of the resident lanes per step of
+// work, ceil(Q (ceil(D / L) - 1) / lanes) (L + init).  A part-filled last
+// round costs a whole one there: b40 1e8 (13 super-blocks) takes 0.227 ms at
+// L = 65 (1.95 rounds), 0.270 at L = 63 (2.01) and 0.259 at 61 (2.08); 9e7 is
+// best at 61 (1.76 rounds; profiles/r05/sib_small_L.log).  Sets `rounds`.
+template <class P>
+static u64 pick_small_stride(u128 start, u64 count, u64 lo, u64 hi, int first_limb, u64 Q, u64 lanes, u64 D,
+                             double &rounds, double init = 6, double tol = 6) {
+    const ConflictModel<P> m((long double)start, (long double)count, first_limb);
+    double cost[512];
+    int nc = 0;
+    double min_cost = 1e30;
+    for (u64 L = lo | 1; L <= hi && nc < 512; L += 2, nc++) {
+        cost[nc] = m.cost(L);
+        min_cost = std::min(min_cost, cost[nc]);
+    }
+    u64 best = lo | 1;
+    double best_t = 1e300;
+    rounds = 0;
+    nc = 0;
+    for (u64 L = lo | 1; L <= hi && nc < 512; L += 2, nc++) {
+        if (cost[nc] > min_cost + tol) continue;
+        const u64 units = Q * ((D + L - 1) / L - 1);
+        const double t = (double)((units + lanes - 1) / lanes) * ((double)L + init);
+        if (t < best_t) {
+            best_t = t;
+            best = L;
+            rounds = (double)units / (double)lanes;
+        }
+    }
+    return best;
+}
+
 template <class P>
 static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s) {
     if constexpr (P::SIB > 1) return launch_sib<P>(p, num_cus, s);
@@ -2103,18 +2138,8 @@ static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s
     const int per_cu = per_cu_q < 1 ? 1 : per_cu_q;
     constexpr u64 D = (u64)P::B * P::B, SB = (u64)P::SIB * D;
     const u64 lanes = (u64)num_cus * per_cu * P::WG;
-    // Too short for the sibling walk to pay: the same base without siblings.
-    // Fewer than 3 rounds of the resident lanes' units (at the target
-    // stride; decided before the stride pick, whose ~20 us of host work
-    // would otherwise delay the fallback's launch): the part-filled last
-    // round of the 4-wave grid and the stride's luck decide (b40 1e8: 0.227
-    // ms at L = 65, 1.95 rounds; 0.266 at L = 81, 1.57; the regular kernel
-    // 0.244; at 1e8-1.25e8 the two kernels trade +-6 %, from 2.5e8 the
-    // sibling kernel wins by 6-17 %: profiles/r05/sib_small_l.log,
-    // picker_rounds.log, sib_threshold.log, sib_final_thr.log).
-    if (p.count < 4 * SB ||
-        10 * (p.count / SB) * (D / P::TCHUNK) < (u64)probe_knob("NICE_FD2_SIBROUNDS", 30) * lanes)
-        return launch_cfg<typename P::NoSib>(p, num_cus, s);
+    // too short for the sibling walk to pay: the same base without siblings
+    if (p.count < 4 * SB) return launch_cfg<typename P::NoSib>(p, num_cus, s);
     if (p.cutoff + 1 < (u32)(P::W0 + P::W)) return hipErrorInvalidValue;
     const uint4 *tabs = nullptr;
     hipError_t e = fd2_tables<P>(s, &tabs);
@@ -2123,6 +2148,19 @@ static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s
     // 32 distinct bank pairs (as launch_cfg's chunks).
     const u128 seg_start = ((u128)p.start_hi << 64) | p.start_lo;
     u64 L = probe_knob("NICE_FD2_SIBCHUNK", 0);
+    // Fields of fewer than 3 rounds of the resident lanes' units at the
+    // target stride: the part-filled last round of the 4-wave grid decides,
+    // so the stride fills rounds (pick_small_stride), and below ~1.5 rounds
+    // the regular kernel's finer grid wins (b40 1e8: sibling 0.227-0.239 ms
+    // at L = 65 against 0.242-0.265 regular, 1.25e8 0.263-0.289 against
+    // 0.282-0.307; 9e7 ties; profiles/r05/sib_small_L.log).
+    const u64 Q0 = p.count / SB;
+    if (!L && 10 * Q0 * (D / P::TCHUNK) < 30 * lanes) {
+        double rounds = 0;
+        L = pick_small_stride<P>(seg_start, p.count, P::TCHUNK * 3 / 4, P::TCHUNK, P::LO + 1, Q0, lanes, D, rounds);
+        if (10 * rounds < (double)probe_knob("NICE_FD2_SIBROUNDS", 15))
+            return launch_cfg<typename P::NoSib>(p, num_cus, s);
+    }
     if (!L) L = pick_lane_stride<P>(seg_start, p.count, P::TCHUNK * 3 / 4, P::TCHUNK * 3 / 2, P::TCHUNK, P::LO + 1);
     if (L % 2 == 0) L++;
     if (L > D / 4) L = (D / 4) | 1;
