@@ -2148,16 +2148,19 @@ static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s
     // 32 distinct bank pairs (as launch_cfg's chunks).
     const u128 seg_start = ((u128)p.start_hi << 64) | p.start_lo;
     u64 L = probe_knob("NICE_FD2_SIBCHUNK", 0);
-    // Fields of fewer than 3 rounds of the resident lanes' units at the
+    // Fields of fewer than 6 rounds of the resident lanes' units at the
     // target stride: the part-filled last round of the 4-wave grid decides,
-    // so the stride fills rounds (pick_small_stride), and below ~1.5 rounds
-    // the regular kernel's finer grid wins (b40 1e8: sibling 0.227-0.239 ms
-    // at L = 65 against 0.242-0.265 regular, 1.25e8 0.263-0.289 against
-    // 0.282-0.307; 9e7 ties; profiles/r05/sib_small_L.log).
+    // so the stride fills rounds (pick_small_stride over [60, 100]), and
+    // below ~1.5 rounds the regular kernel's finer grid wins (b40 1e8:
+    // sibling 0.227-0.239 ms at L = 65 against 0.242-0.265 regular, 1.25e8
+    // 0.263-0.289 against 0.282-0.307; 9e7 ties; profiles/r05/
+    // sib_small_L.log; the 4- and 8-way shards of the bench field,
+    // shard_projection.log).
     const u64 Q0 = p.count / SB;
-    if (!L && 10 * Q0 * (D / P::TCHUNK) < 30 * lanes) {
+    if (!L && 10 * Q0 * (D / P::TCHUNK) < 60 * lanes) {
         double rounds = 0;
-        L = pick_small_stride<P>(seg_start, p.count, P::TCHUNK * 3 / 4, P::TCHUNK, P::LO + 1, Q0, lanes, D, rounds);
+        L = pick_small_stride<P>(seg_start, p.count, P::TCHUNK * 3 / 4, P::TCHUNK * 5 / 4, P::LO + 1, Q0, lanes, D,
+                                 rounds);
         if (10 * rounds < (double)probe_knob("NICE_FD2_SIBROUNDS", 15))
             return launch_cfg<typename P::NoSib>(p, num_cus, s);
     }
