@@ -28,16 +28,25 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
                               lds_bytes(B_, big_wg(B_)),
                       "lds_bytes mirrors Cfg");
 #include NICE_PROBE_INC("fd2_part_probe_dispatch.inc")
-        // b40 fields >= 1e7: three sibling lanes (Cfg::SIB, fd2_kernel.hpp):
-        // on the first limb layout (the range's first ~29 %, the benchmark
-        // fields) pipelined with the lowest C limb above the shared one
-        // decoded by VALU, elsewhere per-sibling lookup groups, no VALU decode
-        // (profiles/r05/sib_sweep_range.log)
+        // b40 fields >= 1e7: three sibling lanes (Cfg::SIB, fd2_kernel.hpp;
+        // launch_sib falls back to the regular kernel below ~1.5 rounds of
+        // sibling units): on the first limb layout (the range's first ~29 %,
+        // the benchmark fields) pipelined with the lowest C limb above the
+        // shared one decoded by VALU, elsewhere per-sibling lookup groups, no
+        // VALU decode (profiles/r05/sib_sweep_range.log)
         if constexpr (B_ == 40) {
             if (!wg512) {
                 if constexpr (ND_ == 4) return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, 4097, 100, 0, 3>>(p, num_cus, s);
                 else return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, 0, 1, 0, 3>>(p, num_cus, s);
             }
+        }
+        // b42..45 the same, per-sibling lookup groups: 1e9 at the range start
+        // and half-way b42 -11 / -8 %, b43 -12 / -14, b44 -10 / -11, b45 -6 /
+        // -3 against their regular kernels; b47 +1..+3 and b48-52 +10..+25
+        // (their larger tables leave one workgroup per CU, 2 waves per SIMD),
+        // so they keep the regular kernel (profiles/r05/sib_bases_ab.log)
+        if constexpr (B_ >= 42 && B_ <= 45) {
+            if (!wg512) return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, 0, 1, 0, 3>>(p, num_cus, s);
         }
         // (the LSDX bases' tables leave room for one workgroup per CU: 1024
         // threads for every field size, 4 waves per SIMD instead of 2)

@@ -19,14 +19,22 @@ using namespace nice::fd2;
 #ifndef XPROBE
 #define XPROBE 0
 #endif
-// XREF 0: the round-4 kernel; 1: the round-5 production sibling kernel
+// XB / XND / XNE / XNE2: base and limb combo (default b40 4 8 5)
+#ifndef XB
+#define XB 40
+#define XND 4
+#define XNE 8
+#define XNE2 5
+#endif
+// XREF 0: the regular big-field kernel of the base (b40: the round-4
+// kernel); 1: the round-5 production b40 sibling kernel
 #if defined(XREF) && XREF == 1
 using Ref = Cfg<40, 4, 8, 5, 0, 512, 4097, 100, 0, 3>;
 #else
 #define XREF 0
-using Ref = Cfg<40, 4, 8, 5, 0, 1024, 2049>;
+using Ref = Cfg<XB, XND, XNE, XNE2, 0, big_wg(XB), valu_limbs_big(XB, XND, XNE)>;
 #endif
-using Var = Cfg<40, 4, 8, 5, XPROBE, XWG, XVD, XLG, 0, XM>;
+using Var = Cfg<XB, XND, XNE, XNE2, XPROBE, XWG, XVD, XLG, 0, XM>;
 
 template <class P>
 static double run(u64 start, u64 count, std::vector<u64> &hist, u32 &nmiss, int reps) {
@@ -50,8 +58,8 @@ static double run(u64 start, u64 count, std::vector<u64> &hist, u32 &nmiss, int 
         DetailedLaunch p{};
         p.start_lo = start;
         p.count = count;
-        p.base = 40;
-        p.cutoff = 36;
+        p.base = XB;
+        p.cutoff = (u32)(XB * 9 / 10);  // floor(b * 0.9) (number_stats.rs:15-17; exact for these bases)
         p.hist = d_hist;
         p.hist_copies = kHistCopies;
         p.out = NumOut{d_n, d_u, d_count, 1u << 20};
@@ -103,9 +111,9 @@ int main(int argc, char **argv) {
             bad++;
         }
     }
-    printf("REF=%d PROBE=%d M=%d WG=%d VD=%d LG=%d start=%llu count=%llu: ref %.1f us var %.1f us, sums %llu %llu, "
+    printf("B=%d REF=%d PROBE=%d M=%d WG=%d VD=%d LG=%d start=%llu count=%llu: ref %.1f us var %.1f us, sums %llu %llu, "
            "near-miss %u %u, %s\n",
-           XREF, XPROBE, XM, XWG, XVD, XLG, (unsigned long long)start, (unsigned long long)count, t0 * 1e3, t1 * 1e3,
+           XB, XREF, XPROBE, XM, XWG, XVD, XLG, (unsigned long long)start, (unsigned long long)count, t0 * 1e3, t1 * 1e3,
            (unsigned long long)s0, (unsigned long long)s1, m0, m1, bad || m0 != m1 ? "MISMATCH" : "match");
     return bad || m0 != m1;
 }

@@ -1259,8 +1259,9 @@ def test_eight_shard_context():
         c.close()
 
 
-@pytest.mark.parametrize("frac", [0.0, 0.1, 0.2926, 0.45, 0.97])
-def test_sibling_kernel_equals_small_fields(ctx, frac):
+@pytest.mark.parametrize("base,frac", [(40, 0.0), (40, 0.1), (40, 0.2926), (40, 0.45), (40, 0.97),
+                                       (42, 0.0), (43, 0.6), (44, 0.3), (45, 0.0), (45, 0.8)])
+def test_sibling_kernel_equals_small_fields(ctx, base, frac):
     """b40 fields of >= ~1.9e8 numbers (3 rounds of the resident lanes' units,
     launch_sib) run the sibling-lane kernel (Cfg::SIB = 3, fd2_kernel.hpp: a
     lane steps n, n + B^2 and n + 2 B^2 together, sharing limbs 0 and 1;
@@ -1268,27 +1269,28 @@ def test_sibling_kernel_equals_small_fields(ctx, frac):
     the regular remainder in one launch; the lane stride from the
     bank-conflict model).  Shorter fields run the round-4 kernel (512 threads
     below 1e7).  A field of ragged size at several points of the range
-    (0.2926: across the limb-count cut at 2n + 1 = 40^8) must equal the sum of
-    its sub-1e7 pieces, and every near-miss must recompute by the oracle."""
-    r0, r1 = O.base_range(40)
+    (b40 0.2926: across the limb-count cut at 2n + 1 = 40^8) must equal the
+    sum of its sub-1e7 pieces, and every near-miss must recompute by the
+    oracle.  b42..45 run the same kernel (per-sibling lookup groups)."""
+    r0, r1 = O.base_range(base)
     s = r0 + int((r1 - r0) * frac) + 12345
-    n = 26 * 3 * 1600 ** 2 + 2_345_677  # 26 super-blocks (2.0e8) + a remainder
+    n = 26 * 3 * (base * base) ** 2 + 2_345_677  # 26 super-blocks + a remainder
     if s + n > r1:
         s = r1 - n
-    h, l = ctx.detailed_raw(s, s + n, 40)
+    h, l = ctx.detailed_raw(s, s + n, base)
     assert sum(h) == n
     piece = 9_000_001
     hs, ls = [0] * len(h), []
     a = s
     while a < s + n:
         b = min(s + n, a + piece)
-        hk, lk = ctx.detailed_raw(a, b, 40)
+        hk, lk = ctx.detailed_raw(a, b, base)
         hs = [x + y for x, y in zip(hs, hk)]
         ls += lk
         a = b
     assert h == hs and l == ls
-    assert all(O.num_unique_digits(m, 40) == u for m, u in l)
+    assert all(O.num_unique_digits(m, base) == u for m, u in l)
     # a window of the same field against the oracle itself
-    want = O.process_range_detailed(s, s + 200_003, 40)
-    hw, lw = ctx.detailed_raw(s, s + 200_003, 40)
+    want = O.process_range_detailed(s, s + 200_003, base)
+    hw, lw = ctx.detailed_raw(s, s + 200_003, base)
     assert _dist(hw) == want.distribution and lw == want.nice_numbers
