@@ -334,8 +334,13 @@ struct Cfg {
     static constexpr bool LSDX = MW == 2 && DB > 0 && !LSD_W1 && (VD_ & 1024) != 0;
     static constexpr bool LSD = LSD_W1 || LSDX;
     // (regions padded to 16 bytes: the image is copied in with 16-byte accesses)
-    static constexpr int TL = TB + ((int)(B * ES) + 15) / 16 * 16;  // low-digit table (2B entries)
-    static constexpr int TK = TL + (LSD ? ((int)(2 * B * ES) + 15) / 16 * 16 : 0);  // LSDX: carry bytes
+    static constexpr int TL = TB + ((int)(B * ES) + 15) / 16 * 16;  // low-digit table (LDE entries)
+    // Low-digit entries: a lane whose chunk starts at n reads n mod B + i, i <
+    // chunk <= B, so 2B cover any chunk.  The sibling kernels of b46+ keep
+    // B + 256 (their chunks are capped at 256, launch_sib): the table then
+    // leaves room for two 512-thread workgroups per CU.
+    static constexpr int LDE = (SIB_ > 1 && BASE_ >= 46) ? (int)B + 256 : 2 * (int)B;
+    static constexpr int TK = TL + (LSD ? ((int)(LDE * ES) + 15) / 16 * 16 : 0);  // LSDX: carry bytes
     static constexpr int TEND = SPLIT ? (TB + (int)(B * ES) + 15) / 16 * 16
                                       : TK + (LSDX ? ((int)(2 * B) + 15) / 16 * 16 : 0);
     static constexpr int HB = SPLIT ? TEND : 0;  // window rows
@@ -422,8 +427,12 @@ struct Cfg {
     // the workgroup size rounds prefer
     using NoPers = Cfg<BASE_, ND_, NE_, NE2_, PROBE_, (PERS_ < 0 ? rounds_wg(BASE_) : WG_), VD_, LG_, 0>;
     // the production kernel without sibling lanes (segments shorter than a
-    // few M B^2): the big-field workgroup size and VALU-decoded limbs
-    using NoSib = Cfg<BASE_, ND_, NE_, NE2_, PROBE_, rounds_wg(BASE_), valu_limbs_big(BASE_, ND_, NE_), -1, 0>;
+    // few M B^2): the big-field workgroup size and VALU-decoded limbs; b46+
+    // keep the persistent-grid default of their regular kernel (b52..55 1e8
+    // fields: rounds of workgroups +8..+10 %, profiles/r05/sib_short_table_ab.log)
+    using NoSib = std::conditional_t<(BASE_ >= 46),
+                                     Cfg<BASE_, ND_, NE_, NE2_, PROBE_, big_wg(BASE_), valu_limbs_big(BASE_, ND_, NE_)>,
+                                     Cfg<BASE_, ND_, NE_, NE2_, PROBE_, rounds_wg(BASE_), valu_limbs_big(BASE_, ND_, NE_), -1, 0>>;
     // lookup groups of walk_chunk (the sibling kernel's regular parts: none)
     static constexpr int LGW = SIB_ > 1 ? 0 : (LG_ >= 0 ? LG_ : (MW == 3 && WG_ >= 1024 ? 8 : 0));
     // VD & 256 (no low-digit table only): limb 0 of S and of C by VALU too --
@@ -920,7 +929,7 @@ __global__ void fd2_tables_kernel(unsigned char *tb) {
             v[1] |= f;
         }
         put(tb + (P::TL - P::TC0) + e * P::ES);
-        put(tb + (P::TL - P::TC0) + (e + P::B) * P::ES);
+        if ((int)(e + P::B) < P::LDE) put(tb + (P::TL - P::TC0) + (e + P::B) * P::ES);
     }
 }
 
@@ -2165,8 +2174,11 @@ static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s
             return launch_cfg<typename P::NoSib>(p, num_cus, s);
     }
     if (!L) L = pick_lane_stride<P>(seg_start, p.count, P::TCHUNK * 3 / 4, P::TCHUNK * 3 / 2, P::TCHUNK, P::LO + 1);
+    // chunks reach low-digit entries n mod B + i < LDE (Cfg::LDE)
+    constexpr u64 LMAX = (u64)P::LDE - P::B;
     if (L % 2 == 0) L++;
     if (L > D / 4) L = (D / 4) | 1;
+    if (L > LMAX) L = LMAX % 2 ? LMAX : LMAX - 1;
     const u64 U = (D + L - 1) / L, r = D - (U - 1) * L;
     const bool has_edge = r != L;
     const u64 upb = has_edge ? U - 1 : U;
@@ -2196,7 +2208,7 @@ static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s
             if (chunk < 4) chunk = R < 4 ? R : 4;
             if (chunk < 1) chunk = 1;
             if (chunk > 1 && chunk % 2 == 0) chunk++;
-            if (chunk > P::B) chunk = P::B % 2 ? P::B : P::B - 1;
+            if (chunk > LMAX) chunk = LMAX % 2 ? LMAX : LMAX - 1;
             nunits = R / chunk;
             tail = R - nunits * chunk;
         }

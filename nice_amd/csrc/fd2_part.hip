@@ -42,11 +42,17 @@ static hipError_t try_combo(const DetailedLaunch &p, int nd, int ne, int ne2, bo
         }
         // b42..45 the same, per-sibling lookup groups: 1e9 at the range start
         // and half-way b42 -11 / -8 %, b43 -12 / -14, b44 -10 / -11, b45 -6 /
-        // -3 against their regular kernels; b47 +1..+3 and b48-52 +10..+25
-        // (their larger tables leave one workgroup per CU, 2 waves per SIMD),
-        // so they keep the regular kernel (profiles/r05/sib_bases_ab.log)
+        // -3 against their regular kernels (profiles/r05/sib_bases_ab.log)
         if constexpr (B_ >= 42 && B_ <= 45) {
             if (!wg512) return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, 0, 1, 0, 3>>(p, num_cus, s);
+        }
+        // b47..55: two sibling lanes over the short low-digit table (Cfg::LDE,
+        // two 512-thread workgroups per CU; with the full 2B table and three
+        // lanes they held one and lost +1..+25 %): 1e9 at the range start and
+        // half-way -2..-9 %, b50 / b53 half-way -2 / -0.6 %
+        // (profiles/r05/sib_short_table_ab.log)
+        if constexpr (B_ >= 47 && B_ <= 55 && B_ != 51) {
+            if (!wg512) return launch_cfg<Cfg<B_, ND_, NE_, NE2_, 0, 512, 0, 1, 0, 2>>(p, num_cus, s);
         }
         // (the LSDX bases' tables leave room for one workgroup per CU: 1024
         // threads for every field size, 4 waves per SIMD instead of 2)

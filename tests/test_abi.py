@@ -273,12 +273,15 @@ def test_product_library_has_no_probe_kernels():
     # neither the split b64 + u16 table layout (VD & 512) nor a forced lookup
     # grouping (the per-base default is -1) is a product variant; PERS is the
     # per-base default (-1) or the rounds fallback of a persistent kernel (0).
-    # The sibling-lane kernels (SIB > 1, b40..45) name their walk explicitly:
-    # LG 1 (per-sibling lookup groups) or 100 (the software-pipelined walk)
+    # The sibling-lane kernels name their walk explicitly: three lanes on
+    # b40..45 with LG 1 (per-sibling lookup groups) or 100 (the software-
+    # pipelined walk), two lanes on b47..55 (short low-digit table) with LG 1
     for c in cfgs:
         assert c[6] & 512 == 0 and c[8] in (-1, 0), c
-        assert c[7] == -1 if c[9] <= 1 else (40 <= c[0] <= 45 and c[9] == 3 and c[7] in (1, 100)), c
-    assert any(c[9] == 3 for c in cfgs), "no sibling-lane kernel"
+        assert c[7] == -1 if c[9] <= 1 else ((40 <= c[0] <= 45 and c[9] == 3 and c[7] in (1, 100))
+                                             or (47 <= c[0] <= 55 and c[9] == 2 and c[7] == 1)), c
+    assert any(c[9] == 3 for c in cfgs), "no three-lane sibling kernel"
+    assert any(c[9] == 2 for c in cfgs), "no two-lane sibling kernel"
     assert "detailed_fd_kernel" not in syms
     with open(_lib.LIB_PATH, "rb") as f:
         blob = f.read()

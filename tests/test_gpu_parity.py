@@ -1260,7 +1260,9 @@ def test_eight_shard_context():
 
 
 @pytest.mark.parametrize("base,frac", [(40, 0.0), (40, 0.1), (40, 0.2926), (40, 0.45), (40, 0.97),
-                                       (42, 0.0), (43, 0.6), (44, 0.3), (45, 0.0), (45, 0.8)])
+                                       (42, 0.0), (43, 0.6), (44, 0.3), (45, 0.0), (45, 0.8),
+                                       (47, 0.0), (48, 0.5), (49, 0.3), (50, 0.5), (52, 0.2),
+                                       (53, 0.5), (54, 0.6), (55, 0.0), (55, 0.8)])
 def test_sibling_kernel_equals_small_fields(ctx, base, frac):
     """b40 fields of >= ~1.9e8 numbers (3 rounds of the resident lanes' units,
     launch_sib) run the sibling-lane kernel (Cfg::SIB = 3, fd2_kernel.hpp: a
@@ -1271,10 +1273,13 @@ def test_sibling_kernel_equals_small_fields(ctx, base, frac):
     below 1e7).  A field of ragged size at several points of the range
     (b40 0.2926: across the limb-count cut at 2n + 1 = 40^8) must equal the
     sum of its sub-1e7 pieces, and every near-miss must recompute by the
-    oracle.  b42..45 run the same kernel (per-sibling lookup groups)."""
+    oracle.  b42..45 run the same kernel (per-sibling lookup groups), b47..55
+    two lanes (Cfg::SIB = 2) over the short low-digit table (Cfg::LDE: lane
+    strides capped at 255)."""
     r0, r1 = O.base_range(base)
     s = r0 + int((r1 - r0) * frac) + 12345
-    n = 26 * 3 * (base * base) ** 2 + 2_345_677  # 26 super-blocks + a remainder
+    m = 3 if base <= 45 else 2
+    n = 26 * m * (base * base) ** 2 + 2_345_677  # 26 super-blocks + a remainder
     if s + n > r1:
         s = r1 - n
     h, l = ctx.detailed_raw(s, s + n, base)
