@@ -238,6 +238,48 @@ def cpu_baseline(start, target_s, base=BASE, field=FIELD_SIZE):
             "detailed_numbers_per_sec": det_rate, "niceonly_numbers_per_sec": nice_rate}
 
 
+def fixture_check(field, base, mode, res, world=1):
+    """The last timed field's results against the committed oracle fixture of
+    this exact field (tests/golden/oracle_fields.json, data only -- the
+    oracle is not run here): the detailed distribution and near-miss list,
+    and the niceonly stride-candidate count and nice list.  None when no
+    fixture holds this field (non-default configs).  Over N > 1 ranks the
+    histogram and the lists are the exchanged whole-field ones; the candidate
+    count is rank 0's dealt share, so it is not compared there."""
+    path = os.path.join(ROOT, "tests", "golden", "oracle_fields.json")
+    try:
+        with open(path) as f:
+            fx = json.load(f)
+    except OSError:
+        return None
+    key = (str(field.range_start), str(field.range_end), base)
+    det_fx = [d for d in fx["detailed"] if (d["start"], d["end"], d["base"]) == key]
+    nice_fx = [d for d in fx["niceonly"] if (d["start"], d["end"], d["base"]) == key]
+    _, det, nic, st = res
+    out = {"fixture": "tests/golden/oracle_fields.json"}
+    ok = True
+    if mode in ("both", "detailed"):
+        if not det_fx:
+            return None
+        d = det_fx[0]
+        dist_ok = [(x.num_uniques, x.count) for x in det.distribution] == [tuple(v) for v in d["distribution"]]
+        near_ok = [(n.number, n.num_uniques) for n in det.nice_numbers] == [(int(n), u) for n, u in d["near_misses"]]
+        out["detailed"] = {"name": d["name"], "distribution": dist_ok, "near_misses": near_ok,
+                           "near_miss_count": len(d["near_misses"])}
+        ok = ok and dist_ok and near_ok
+    if mode in ("both", "niceonly"):
+        if not nice_fx or st is None:
+            return None
+        d = nice_fx[0]
+        cand_ok = st.candidates == d["candidates"] if world == 1 else None
+        list_ok = [str(n.number) for n in nic.nice_numbers] == d["nice_numbers"]
+        out["niceonly"] = {"name": d["name"], "candidates": st.candidates, "candidates_match": cand_ok,
+                           "nice_numbers": list_ok}
+        ok = ok and cand_ok is not False and list_ok
+    out["verified"] = ok
+    return out
+
+
 def main(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -293,6 +335,7 @@ def main(args):
             det_ctx.synchronize()
 
     last_stats = [None]
+    last_res = [None]  # the last field's whole results (fixture_check after the timed region)
     checked = [0]  # fields whose whole-field results came back and were checked
 
     def check(res):
@@ -301,6 +344,7 @@ def main(args):
             assert sum(d.count for d in det.distribution) == job_size
         checked[0] += 1
         last_stats[0] = st or last_stats[0]
+        last_res[0] = res
 
     def make_pipeline(d):
         # detailed-only / niceonly-only runs pass a context that skips the other mode
@@ -354,6 +398,8 @@ def main(args):
     checked[0] = 0
     elapsed = timed(step, args.steps, barrier_sync, dist, tail=tail)
     fields_checked = checked[0]  # every field of the timed region came back whole and was checked
+    # the timed region's last field against the oracle fixture of this field
+    fixture = fixture_check(field, base, args.mode, last_res[0], world) if last_res[0] is not None else None
     # Event spans of the detailed launches inside the timed region: consecutive
     # fields run on different slots' streams and overlap at their edges by
     # design (a field's first workgroups fill the CUs the previous field's last
@@ -465,6 +511,9 @@ def main(args):
         },
     }
     line["fields_checked"] = fields_checked
+    line["verified_against_fixture"] = bool(fixture and fixture["verified"])
+    if fixture is not None:
+        line["fixture_check"] = fixture
     for name, el in per_mode.items():
         line[f"{name}_numbers_per_sec"] = job_size * args.steps / el
         line[f"{name}_ms_per_step"] = el / args.steps * 1e3

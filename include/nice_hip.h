@@ -73,9 +73,11 @@ const char *nice_last_error(void);
  * the client's tasks behind a Mutex, client/src/main.rs:622,
  * client_process_gpu.rs:199-200): when every slot holds a field in flight the
  * call blocks until another thread's collect frees one.  It returns
- * NICE_ERR_BUSY instead only when no other thread could free a slot (every
- * field in flight was submitted by the calling thread and is not being
- * collected), which would otherwise deadlock. */
+ * NICE_ERR_BUSY instead only when no other thread could free a slot, which
+ * would otherwise deadlock: no field in flight is being collected, and each
+ * was submitted by the calling thread or by a thread that is itself blocked
+ * in such a call (two threads holding tickets and waiting for each other's
+ * slots: the second to call gets NICE_ERR_BUSY). */
 int nice_process_range_detailed(nice_ctx *ctx, uint64_t start_lo, uint64_t start_hi,
                                 uint64_t end_lo, uint64_t end_hi, uint32_t base,
                                 uint64_t *hist, nice_number *out, size_t cap, size_t *n_out);
@@ -228,6 +230,8 @@ typedef struct {
     uint32_t launches;
     uint32_t fd_kernel;  /* 1 if the finite-difference kernel ran */
     uint64_t numbers;    /* numbers processed by those launches */
+    uint32_t sib_lanes;  /* sibling lanes M of the FD kernel's last sibling-lane launch (0: none ran) */
+    uint32_t sib_stride; /* ... and its lane stride L */
 } nice_kernel_stats;
 int nice_last_kernel_stats(nice_ctx *ctx, int device_index, nice_kernel_stats *out);
 /* Kernel timing of later detailed fields on this context (default on): with
@@ -239,9 +243,19 @@ int nice_ctx_set_kernel_timing(nice_ctx *ctx, int enable);
 
 /* Host helpers mirroring the reference functions the client calls. */
 /* std::thread::available_parallelism() (client_process_gpu.rs:598): the
- * process's CPU affinity mask, capped by a cgroup v2 cpu.max quota.  The
- * host MSD pool's size when nice_niceonly_opts.threads is 0. */
+ * process's CPU affinity mask, capped by the cgroup v2 cpu.max quotas of its
+ * cgroup and the cgroup's ancestors (quota / period rounded down, at least 1,
+ * as Rust's std does).  The host MSD pool's size when
+ * nice_niceonly_opts.threads is 0. */
 uint32_t nice_host_threads(void);
+/* Test hook: every later sibling-lane launch of the FD kernel in this
+ * process uses lane stride L (odd, <= 255) instead of the bank-conflict
+ * model's pick, and fields of >= 4 super-blocks take the sibling kernel
+ * whatever their size; 0 restores production.  NICE_ERR_INVALID otherwise. */
+int nice_debug_force_sib_stride(uint32_t L);
+/* Test hook: the cpu.max cap nice_host_threads applies for the cgroup
+ * `cgroup_path` under a cgroup2 mount at `root` (0 = no quota). */
+uint32_t nice_debug_cgroup_cpus(const char *root, const char *cgroup_path);
 /* get_base_range_u128 (base_range.rs:43-54): 1 range, 0 none, -1 exceeds u128. */
 int nice_base_range(uint32_t base, uint64_t *start_lo, uint64_t *start_hi, uint64_t *end_lo,
                     uint64_t *end_hi);

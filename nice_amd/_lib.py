@@ -37,7 +37,7 @@ EXPORTS = (
     "nice_detailed_collect", "nice_niceonly_submit", "nice_niceonly_collect",
     "nice_cpu_process_range_detailed", "nice_cpu_process_range_niceonly",
     "nice_adaptive_floor_step", "nice_adaptive_floor", "nice_ctx_set_kernel_timing",
-    "nice_host_threads",
+    "nice_host_threads", "nice_debug_cgroup_cpus", "nice_debug_force_sib_stride",
 )
 
 
@@ -73,7 +73,8 @@ class nice_niceonly_stats(ctypes.Structure):
 
 class nice_kernel_stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("launches", ctypes.c_uint32),
-                ("fd_kernel", ctypes.c_uint32), ("numbers", ctypes.c_uint64)]
+                ("fd_kernel", ctypes.c_uint32), ("numbers", ctypes.c_uint64),
+                ("sib_lanes", ctypes.c_uint32), ("sib_stride", ctypes.c_uint32)]
 
 
 _lib = None
@@ -142,6 +143,8 @@ def lib():
         "nice_adaptive_floor_step": ([ctypes.c_double, ctypes.c_double, ctypes.c_double], ctypes.c_double),
         "nice_adaptive_floor": ([ctypes.POINTER(ctypes.c_double), P32], i32),
         "nice_host_threads": ([], u32),
+        "nice_debug_cgroup_cpus": ([ctypes.c_char_p, ctypes.c_char_p], u32),
+        "nice_debug_force_sib_stride": ([u32], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -152,6 +152,8 @@ class KernelStats:
     launches: int
     fd_kernel: bool
     numbers: int
+    sib_lanes: int = 0   # sibling lanes of the FD kernel's last sibling launch (0: none)
+    sib_stride: int = 0  # ... and its lane stride
 
 
 class GpuContext:
@@ -205,7 +207,7 @@ class GpuContext:
     def kernel_stats(self, device_index: int = 0) -> KernelStats:
         s = _lib.nice_kernel_stats()
         check(lib().nice_last_kernel_stats(self._h, device_index, s))
-        return KernelStats(s.kernel_ms, s.launches, bool(s.fd_kernel), s.numbers)
+        return KernelStats(s.kernel_ms, s.launches, bool(s.fd_kernel), s.numbers, s.sib_lanes, s.sib_stride)
 
     # -- detailed -------------------------------------------------------------
     def detailed_raw(self, start: int, end: int, base: int, cap: int = 0):

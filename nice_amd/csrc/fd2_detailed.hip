@@ -13,6 +13,7 @@ namespace nice {
 namespace fd2 {
 
 NICE_PROBE_ONLY(u64 *g_stamps = nullptr; u64 g_last_launch[6] = {};)  // phase stamps, last launch (probe build)
+std::atomic<uint32_t> g_force_sib_stride{0};  // nice_debug_force_sib_stride
 
 // ---------------------------------------------------------------------------
 // Host: limb counts per segment.  For a segment [a, e) the last FD state a
@@ -126,6 +127,8 @@ static hipError_t launch_segment(const DetailedLaunch &p, const Combo &c, int nu
 }
 
 }  // namespace fd2
+
+void fd2_force_sib_stride(uint32_t L) { fd2::g_force_sib_stride.store(L, std::memory_order_relaxed); }
 
 bool fd2_supported(uint32_t base) {
     switch (base) {

@@ -49,6 +49,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <map>
 #include <tuple>
@@ -977,6 +978,8 @@ static hipError_t fd2_tables(hipStream_t s, const uint4 **out) {
 // a stamp compiles to nothing.)
 constexpr u32 kStampGroups = 65536, kStampWords = 32;
 NICE_PROBE_ONLY(extern u64 *g_stamps; extern u64 g_last_launch[6];)  // last launch: grid, WG, chunk, nunits, tail, per_cu
+// Forced sibling lane stride (nice_debug_force_sib_stride; 0: the model's pick).
+extern std::atomic<uint32_t> g_force_sib_stride;
 #define FD2_STAMP_P(p, k)                                                                        \
     do {                                                                                         \
         if (kProbes && (p) && threadIdx.x == 0 && blockIdx.x < kStampGroups) {                   \
@@ -2157,6 +2160,10 @@ static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s
     // 32 distinct bank pairs (as launch_cfg's chunks).
     const u128 seg_start = ((u128)p.start_hi << 64) | p.start_lo;
     u64 L = probe_knob("NICE_FD2_SIBCHUNK", 0);
+    // a stride forced by the test hook also skips the small-field fallback
+    // below (every stride the pickers can return is then reachable on a
+    // field of >= 4 super-blocks)
+    if (!L) L = g_force_sib_stride.load(std::memory_order_relaxed);
     // Fields of fewer than 6 rounds of the resident lanes' units at the
     // target stride: the part-filled last round of the 4-wave grid decides,
     // so the stride fills rounds (pick_small_stride over [60, 100]), and
@@ -2184,6 +2191,10 @@ static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s
     const u64 upb = has_edge ? U - 1 : U;
     // the lanes' u16 window counters hold M L numbers
     if ((u64)P::SIB * L > 65535) return hipErrorInvalidValue;
+    if (p.sib) {
+        p.sib[0] = (uint32_t)P::SIB;
+        p.sib[1] = (uint32_t)L;
+    }
     // Launch bound: unit counts in 32 bits and, as launch_cfg's, 60 000
     // numbers per resident lane -- counted at the regular kernel's 2048 lanes
     // per CU, so a b40 launch still takes up to 3.1e10 numbers whatever the

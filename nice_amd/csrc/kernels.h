@@ -41,6 +41,8 @@ struct DetailedLaunch {
     NumOut out;
     FieldFinish fin;             // fd2 only; see FieldFinish
     uint32_t *launches;          // if set, incremented per kernel launch enqueued
+    uint32_t *sib;               // fd2, if set: [0] sibling lanes M of the field's last sibling-lane
+                                 // launch (0: none ran), [1] its lane stride L
 };
 
 // Production FD kernel (fd2_detailed.hip): bases 40, 50, 80, in-range segments.
@@ -48,6 +50,9 @@ bool fd2_supported(uint32_t base);
 hipError_t launch_detailed_fd2(const DetailedLaunch &p, int num_cus, hipStream_t s);
 // The n where fd2's per-segment limb layout changes (ascending).
 size_t fd2_cuts(uint32_t base, unsigned __int128 *out, size_t cap);
+// Test hook: every later sibling-lane launch of the process uses lane stride
+// L (odd; 0 restores the production pick, fd2_kernel.hpp launch_sib).
+void fd2_force_sib_stride(uint32_t L);
 // Field epilogue on the launch stream: out_mapped[0..128] = the summed
 // histogram copies, out_mapped[129] = *count; copies and counter are zeroed.
 hipError_t launch_detailed_finish(uint64_t *hist, uint32_t *count, uint64_t *out_mapped, hipStream_t s);

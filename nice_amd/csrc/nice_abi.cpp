@@ -149,6 +149,7 @@ struct Slot {
     bool marked = false;          // ... or an untimed end marker (ev_done) on a shared stream
     uint64_t seq = 0;             // last detailed field's sequence number
     uint32_t launches = 0;        // ... and its kernel launches (the finish kernel not counted)
+    uint32_t sib[2] = {0, 0};     // ... and its last sibling-lane launch: lanes M, stride L
     bool fin_seq = false;         // ... and whether its fd2 finish publishes it
     MsdBuf msd;
 };
@@ -229,6 +230,9 @@ struct nice_ctx {
     DetJob det[kSlots];
     NiceJob nice[kSlots];
     int det_next = 0, nice_next = 0;
+    // threads blocked in acquire_slot (either mode): they collect nothing
+    // until they get a slot, so their fields do not count as freeable
+    std::vector<std::thread::id> blocked;
 };
 
 namespace {
@@ -251,23 +255,45 @@ int free_slot(const Job *jobs, int next) {
 // submits: the caller collects one first).  With `wait` (the synchronous
 // reference-shaped calls, which the reference serves behind the context's
 // Mutex, client_process_gpu.rs:199-200), block until another thread's
-// collect frees one -- unless no other thread can: every field in flight was
-// submitted by this thread and nobody is collecting it.
+// collect frees one -- unless no other thread can: a field in flight can be
+// freed only while a collect is waiting for it, or while its submitter is a
+// thread that is not itself blocked here (a blocked thread collects nothing:
+// two threads each holding tickets and each waiting for the other's slot
+// would otherwise wait forever, so one of them gets NICE_ERR_BUSY).
 template <class Job>
 int acquire_slot(nice_ctx *ctx, std::unique_lock<std::mutex> &lock, const Job *jobs, int next, bool wait,
                  const char *mode, int *slot) {
+    const std::thread::id me = std::this_thread::get_id();
+    auto blocked = [&](std::thread::id id) {
+        return id == me || std::find(ctx->blocked.begin(), ctx->blocked.end(), id) != ctx->blocked.end();
+    };
+    auto unblock = [&] {
+        auto it = std::find(ctx->blocked.begin(), ctx->blocked.end(), me);
+        if (it != ctx->blocked.end()) {
+            ctx->blocked.erase(it);
+            ctx->freed.notify_all();
+        }
+    };
     for (;;) {
         const int t = free_slot(jobs, next);
         if (t >= 0) {
+            unblock();
             *slot = t;
             return NICE_OK;
         }
-        bool others = false;
+        bool freeable = false;
         for (int i = 0; i < slots_used(); i++)
-            others |= jobs[i].active && (jobs[i].waiting || jobs[i].owner != std::this_thread::get_id());
-        if (!wait || !others)
+            freeable |= jobs[i].active && (jobs[i].waiting || !blocked(jobs[i].owner));
+        if (!wait || !freeable) {
+            unblock();
             return fail(NICE_ERR_BUSY, std::string("three ") + mode +
                                            " fields already in flight on this context; collect one first");
+        }
+        if (std::find(ctx->blocked.begin(), ctx->blocked.end(), me) == ctx->blocked.end()) {
+            ctx->blocked.push_back(me);
+            // waiters that counted on this thread's fields re-check
+            ctx->freed.notify_all();
+        }
         ctx->freed.wait(lock);
     }
 }
@@ -493,6 +519,7 @@ int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *f
     p.hist = sl.d_state;
     p.out = nice::NumOut{sl.det.n, sl.det.u, sl.d_count, sl.det.cap};
     p.launches = &sl.launches;
+    p.sib = sl.sib;
     *finished = false;
     auto launch = [&](u128 a, u128 b, bool fd) -> int {
         if (a >= b) return NICE_OK;
@@ -640,6 +667,7 @@ int enqueue_detailed_shard(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, b
     }
     sl.seq++;
     sl.launches = 0;
+    sl.sib[0] = sl.sib[1] = 0;
     // The state block is zeroed by the previous field's finish; a memset
     // only after an interrupted field (or the first one).
     if (sl.dirty) HIPCHK(hipMemsetAsync(sl.d_state, 0, kStateBytes, sl.stream));
@@ -714,6 +742,8 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
         d.last.numbers = (uint64_t)(job.bounds[i + 1] - job.bounds[i]);
         d.last.launches = sl.launches;
         d.last.fd_kernel = nice::fd2_supported(base) ? 1u : 0u;
+        d.last.sib_lanes = sl.sib[0];
+        d.last.sib_stride = sl.sib[1];
         uint32_t cnt = (uint32_t)sl.h_fin[129];
         if (cnt > sl.det.cap) {
             // Near-miss list overflowed (e.g. out-of-range n, SURVEY hazard 9):
@@ -726,6 +756,8 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
             sl.dirty = false;
             d.stats_slot = t;
             d.last.launches = sl.launches;
+            d.last.sib_lanes = sl.sib[0];
+            d.last.sib_stride = sl.sib[1];
             cnt = (uint32_t)sl.h_fin[129];
             if (cnt > sl.det.cap) return fail(NICE_ERR_HIP, "near-miss list overflow after resize");
         }
@@ -755,6 +787,20 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
         // stream (so no queued field is waited for), all devices at once.
         std::vector<std::vector<uint32_t>> u(nd);
         std::vector<std::vector<uint64_t>> pairs(nd);
+        // Devices whose aux stream still has copies from / into pairs and u:
+        // any return drains them first (declared after the buffers, so it
+        // runs before they are freed).
+        struct Drain {
+            nice_ctx *ctx;
+            std::vector<char> q;
+            ~Drain() {
+                for (size_t j = 0; j < q.size(); j++)
+                    if (q[j]) {
+                        (void)hipSetDevice(ctx->devs[j].id);
+                        (void)hipStreamSynchronize(ctx->devs[j].aux);
+                    }
+            }
+        } drain{ctx, std::vector<char>(nd, 0)};
         for (size_t i = 0; i < nd; i++) {
             const size_t n = off[i + 1] - off[i];
             if (!n) continue;
@@ -782,6 +828,7 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
                 d.chk_cap = c;
             }
             u[i].resize(n);
+            drain.q[i] = 1;
             hipError_t err = hipMemcpyAsync(d.chk_n, pairs[i].data(), n * 16, hipMemcpyHostToDevice, d.aux);
             if (err == hipSuccess) err = nice::launch_unique_counts(d.chk_n, (uint32_t)n, base, d.chk_u, d.aux);
             if (err == hipSuccess) err = hipMemcpyAsync(u[i].data(), d.chk_u, n * 4, hipMemcpyDeviceToHost, d.aux);
@@ -792,6 +839,7 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
             Device &d = ctx->devs[i];
             HIPCHK(hipSetDevice(d.id));
             const hipError_t err = hipStreamSynchronize(d.aux);
+            drain.q[i] = 0;
             if (err != hipSuccess) return fail(NICE_ERR_HIP, std::string("self-check: ") + hipGetErrorString(err));
             for (size_t q = 0; q < u[i].size(); q++)
                 if (u[i][q] != job.all[off[i] + q].u)
@@ -1228,22 +1276,64 @@ struct AdaptiveFloor {
 };
 std::mutex g_af_mu;
 
-// std::thread::available_parallelism on Linux: the affinity mask, capped by
-// a cgroup v2 cpu.max quota.
+// CPUs a cgroup v2 cpu.max line grants: quota / period rounded DOWN (Rust's
+// cgroups::quota_v2), 0 for "max" or an unreadable line.
+unsigned cpu_max_cpus(const char *text) {
+    char q[32] = {0};
+    unsigned long period = 0;
+    if (!text || sscanf(text, "%31s %lu", q, &period) != 2 || strcmp(q, "max") == 0 || period == 0) return 0;
+    char *end = nullptr;
+    const unsigned long quota = strtoul(q, &end, 10);
+    if (end == q) return 0;
+    const unsigned long c = quota / period;
+    return c > 0xffffffffUL ? 0xffffffffu : (unsigned)c;
+}
+// The tightest cpu.max of the cgroup `rel` (a path below `root`) and of its
+// ancestors up to root, as Rust walks them; 0 if none limits.
+unsigned cgroup_cpus(const std::string &root, std::string rel) {
+    unsigned best = 0;
+    bool limited = false;
+    for (;;) {
+        while (!rel.empty() && rel.back() == '/') rel.pop_back();
+        if (FILE *f = fopen((root + rel + "/cpu.max").c_str(), "r")) {
+            char line[128] = {0};
+            if (fgets(line, sizeof line, f)) {
+                char q[32] = {0};
+                if (sscanf(line, "%31s", q) == 1 && strcmp(q, "max") != 0) {
+                    const unsigned c = cpu_max_cpus(line);
+                    best = limited ? std::min(best, c) : c;
+                    limited = true;
+                }
+            }
+            fclose(f);
+        }
+        if (rel.empty()) break;
+        const size_t p = rel.rfind('/');
+        rel = p == std::string::npos ? std::string() : rel.substr(0, p);
+    }
+    return limited ? std::max(best, 1u) : 0u;
+}
+// std::thread::available_parallelism on Linux (library/std/src/sys/pal/unix/
+// thread.rs): the affinity mask, capped by the cgroup v2 cpu.max quotas of
+// the process's own cgroup (/proc/self/cgroup "0::<path>") and its ancestors
+// under /sys/fs/cgroup, each quota / period rounded down, at least 1.
 unsigned available_parallelism() {
     unsigned n = std::thread::hardware_concurrency();
     cpu_set_t set;
     if (sched_getaffinity(0, sizeof set, &set) == 0 && CPU_COUNT(&set) > 0) n = (unsigned)CPU_COUNT(&set);
-    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
-        char q[32] = {0};
-        unsigned long period = 0;
-        if (fscanf(f, "%31s %lu", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
-            const unsigned long quota = strtoul(q, nullptr, 10);
-            const unsigned c = (unsigned)((quota + period - 1) / period);
-            if (c >= 1 && c < n) n = c;
-        }
+    std::string rel;
+    if (FILE *f = fopen("/proc/self/cgroup", "r")) {
+        char line[4096];
+        while (fgets(line, sizeof line, f))
+            if (strncmp(line, "0::", 3) == 0) {
+                rel = line + 3;
+                while (!rel.empty() && (rel.back() == '\n' || rel.back() == '\r')) rel.pop_back();
+                break;
+            }
         fclose(f);
     }
+    const unsigned c = cgroup_cpus("/sys/fs/cgroup", rel);
+    if (c >= 1 && c < n) n = c;
     return n ? n : 4;
 }
 
@@ -1269,6 +1359,17 @@ double nice_adaptive_floor_step(double floor, double msd_seconds, double total_s
 }
 
 uint32_t nice_host_threads(void) { return available_parallelism(); }
+
+int nice_debug_force_sib_stride(uint32_t L) {
+    if (L && (L % 2 == 0 || L > 255))
+        return fail(NICE_ERR_INVALID, "sibling lane stride must be odd and <= 255 (0: the production pick)");
+    nice::fd2_force_sib_stride(L);
+    return NICE_OK;
+}
+
+uint32_t nice_debug_cgroup_cpus(const char *root, const char *cgroup_path) {
+    return root ? cgroup_cpus(root, cgroup_path ? cgroup_path : "") : 0u;
+}
 
 int nice_adaptive_floor(double *floor, uint32_t *warmup) {
     std::lock_guard<std::mutex> g(g_af_mu);
@@ -1798,11 +1899,12 @@ int niceonly_collect_locked(nice_ctx *ctx, int t, nice_number *out, size_t cap, 
                 rc = fail(NICE_ERR_HIP, "niceonly list overflowed again after growing it to the field's count");
                 break;
             }
-            // Grow EVERY used device's list to the whole field's count and
-            // re-run the field (under the lock: rare).  The host MSD producer
-            // hands batches to devices in the order its threads finish chunks,
-            // so a re-run can put the hits on another device than the first
-            // run did; no device can hold more than the field's total.
+            // Grow EVERY device's list to the whole field's count and re-run
+            // the field (under the lock: rare).  The host MSD producer hands
+            // batches to devices in the order its threads finish chunks (and
+            // the re-run clears job.used), so a re-run can put the hits on a
+            // device the first run never used; no device can hold more than
+            // the field's total.
             uint64_t total = 0;
             for (uint32_t c : counts) total += c;
             if (total > 0xfffff000ull) {
@@ -1810,9 +1912,8 @@ int niceonly_collect_locked(nice_ctx *ctx, int t, nice_number *out, size_t cap, 
                 break;
             }
             for (size_t i = 0; i < ctx->devs.size() && !rc; i++)
-                if (job.used[i])
-                    rc = ensure_listbuf(ctx->devs[i], ctx->devs[i].slot[t].nice, ((uint32_t)total + 4095u) & ~4095u,
-                                        false);
+                rc = ensure_listbuf(ctx->devs[i], ctx->devs[i].slot[t].nice, ((uint32_t)total + 4095u) & ~4095u,
+                                    false);
             if (!rc) rc = niceonly_enqueue(ctx, t, job);
             if (!rc) job.reruns++;
             if (!rc) rc = niceonly_gather(ctx, job, t, counts, &over);

@@ -13,6 +13,7 @@
 
 using namespace nice;
 using namespace nice::fd2;
+std::atomic<uint32_t> nice::fd2::g_force_sib_stride{0};  // (defined by fd2_detailed.hip in the library)
 #ifndef XLG
 #define XLG -1
 #endif

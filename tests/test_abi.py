@@ -443,6 +443,33 @@ def test_host_threads_follow_the_affinity_mask():
     assert int(out.strip()) == 1
 
 
+def test_cgroup_quota_rounds_down_like_rust(tmp_path):
+    """The cgroup cap of nice_host_threads follows Rust's std
+    (available_parallelism -> cgroups::quota_v2): quota / period rounded
+    DOWN, at least 1, the tightest of the process's cgroup and its
+    ancestors; "max" does not limit."""
+    L = _lib.lib()
+
+    def put(rel, text):
+        d = tmp_path / rel
+        d.mkdir(parents=True, exist_ok=True)
+        (d / "cpu.max").write_text(text + "\n")
+
+    root = str(tmp_path).encode()
+    put("", "max 100000")
+    assert L.nice_debug_cgroup_cpus(root, b"") == 0
+    put("a", "150000 100000")          # 1.5 CPUs -> 1 (a ceiling would say 2)
+    assert L.nice_debug_cgroup_cpus(root, b"/a") == 1
+    put("a", "50000 100000")           # 0.5 CPU -> at least 1
+    assert L.nice_debug_cgroup_cpus(root, b"/a") == 1
+    put("b", "1600000 100000")
+    put("b/c", "max 100000")
+    assert L.nice_debug_cgroup_cpus(root, b"/b/c") == 16   # the parent's quota
+    put("b/c", "390000 100000")
+    assert L.nice_debug_cgroup_cpus(root, b"/b/c/") == 3   # the child's, tighter
+    assert L.nice_debug_cgroup_cpus(root, b"/nonexistent") == 0
+
+
 def test_bad_submit_arguments_fail_at_once():
     """A submit with a bad argument answers NICE_ERR_INVALID immediately (no
     context needed to see it); NICE_ERR_BUSY is its own status."""

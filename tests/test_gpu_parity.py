@@ -1199,6 +1199,47 @@ def test_busy_and_invalid_statuses():
         c.close()
 
 
+def test_synchronous_calls_of_two_ticket_holders_do_not_deadlock():
+    """Thread A holds two asynchronous detailed tickets and thread B one, so
+    every slot is in flight; then both call the SYNCHRONOUS entry point.  The
+    first to enter waits for the other's slot; the second must see that the
+    only thread that could free a slot is itself blocked and answer
+    NICE_ERR_BUSY (nice_hip.h), not wait forever.  Once it collects its
+    ticket, the waiting call goes through."""
+    import threading
+    lib = N._lib.lib()
+    ct = N._lib.ctypes
+    c = N.GpuContext(0)
+    s = O.base_range(40)[0]
+    go = threading.Barrier(2)
+    rcs, errors = {}, []
+
+    def worker(name, k0, nt):
+        try:
+            tick = [c.detailed_submit(s + (k0 + k) * 10 ** 6, s + (k0 + k + 1) * 10 ** 6, 40) for k in range(nt)]
+            go.wait()
+            rc, res = _raw_detailed(lib, ct, c._h, s, s + 1000, 40)
+            rcs[name] = rc
+            for x in tick:
+                c.detailed_collect(x, 40)
+            if rc == 0:
+                assert sum(res[0]) == 1000
+        except BaseException as e:
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=("A", 0, 2)), threading.Thread(target=worker, args=("B", 2, 1))]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=60)
+    alive = any(th.is_alive() for th in threads)
+    if not alive:
+        c.close()
+    assert not alive, "synchronous calls deadlocked"
+    assert not errors, errors[0]
+    assert sorted(rcs.values()) == [N._lib.NICE_OK, N._lib.NICE_ERR_BUSY], rcs
+
+
 def test_host_msd_pool_is_available_parallelism(ctx):
     """threads = 0 sizes the host MSD pool with available_parallelism() (the
     affinity mask capped by the cgroup quota), as client_process_gpu.rs:598
@@ -1264,8 +1305,9 @@ def test_eight_shard_context():
                                        (47, 0.0), (48, 0.5), (49, 0.3), (50, 0.5), (52, 0.2),
                                        (53, 0.5), (54, 0.6), (55, 0.0), (55, 0.8)])
 def test_sibling_kernel_equals_small_fields(ctx, base, frac):
-    """b40 fields of >= ~1.9e8 numbers (3 rounds of the resident lanes' units,
-    launch_sib) run the sibling-lane kernel (Cfg::SIB = 3, fd2_kernel.hpp: a
+    """b40 fields of >= ~1e8 numbers (1.5 rounds of the resident lanes'
+    units, launch_sib's NICE_FD2_SIBROUNDS default 15 / 10) run the
+    sibling-lane kernel (Cfg::SIB = 3, fd2_kernel.hpp: a
     lane steps n, n + B^2 and n + 2 B^2 together, sharing limbs 0 and 1;
     super-blocks, edge units where the lane stride does not divide B^2, and
     the regular remainder in one launch; the lane stride from the
@@ -1284,6 +1326,8 @@ def test_sibling_kernel_equals_small_fields(ctx, base, frac):
         s = r1 - n
     h, l = ctx.detailed_raw(s, s + n, base)
     assert sum(h) == n
+    st = ctx.kernel_stats()
+    assert (st.sib_lanes, st.fd_kernel) == (m, True), st  # the sibling kernel ran (not its fallback)
     piece = 9_000_001
     hs, ls = [0] * len(h), []
     a = s
@@ -1299,3 +1343,59 @@ def test_sibling_kernel_equals_small_fields(ctx, base, frac):
     want = O.process_range_detailed(s, s + 200_003, base)
     hw, lw = ctx.detailed_raw(s, s + 200_003, base)
     assert _dist(hw) == want.distribution and lw == want.nice_numbers
+
+
+# --- round 6: every lane stride the sibling pickers can return --------------
+_STRIDE_FIELDS = {}
+
+
+def _stride_field(base, frac):
+    """A field of 4 super-blocks + a ragged remainder (so edge units, whole
+    super-blocks and the regular remainder part all run) at a fraction of the
+    base's range, and its oracle result (computed once per module)."""
+    key = (base, frac)
+    if key not in _STRIDE_FIELDS:
+        m = 3 if base <= 45 else 2
+        r0, r1 = O.base_range(base)
+        s = r0 + int((r1 - r0) * frac) + 777
+        n = 4 * m * (base * base) ** 2 + 1_234_567
+        want = O.process_field_detailed_mt(s, s + n, base, min(16, os.cpu_count() or 1))
+        _STRIDE_FIELDS[key] = (m, s, n, want)
+    return _STRIDE_FIELDS[key]
+
+
+@pytest.mark.parametrize("base,frac,strides", [
+    (40, 0.0, range(45, 121, 2)),                 # the bench layout: pipelined walk, VALU-decoded C2
+    (40, 0.5, (45, 61, 79, 81, 97, 119)),         # the per-sibling lookup-group walk
+    (52, 0.2, range(45, 121, 2)),                 # two lanes over the short low-digit table
+])
+def test_every_sibling_lane_stride(ctx, base, frac, strides):
+    """the sibling kernels pick their lane stride L per
+    launch (pick_lane_stride over odd L in [0.75, 1.5] TCHUNK, pick_small_stride
+    over [0.75, 1.25] TCHUNK, fd2_kernel.hpp), and every L that does not divide
+    B^2 leaves an edge unit per super-block.  With the stride forced through
+    nice_debug_force_sib_stride, each odd L in [45, 120] (b40, M = 3, and b52,
+    M = 2) runs a field of 4 super-blocks plus a ragged remainder -- whole
+    super-blocks, one edge unit each, the regular remainder part -- and must
+    equal the oracle's histogram and near-miss list bit for bit; the kernel
+    stats must show the sibling kernel ran at that L."""
+    lib = N._lib.lib()
+    m, s, n, want = _stride_field(base, frac)
+    bad = []
+    try:
+        for L in strides:
+            assert lib.nice_debug_force_sib_stride(L) == 0
+            h, lst = ctx.detailed_raw(s, s + n, base)
+            st = ctx.kernel_stats()
+            if (st.sib_lanes, st.sib_stride) != (m, L):
+                bad.append((L, "ran", st.sib_lanes, st.sib_stride))
+            elif _dist(h) != want.distribution or lst != want.nice_numbers:
+                bad.append((L, "result"))
+    finally:
+        lib.nice_debug_force_sib_stride(0)
+    assert not bad, bad
+    assert lib.nice_debug_force_sib_stride(2) == N._lib.NICE_ERR_INVALID
+    assert lib.nice_debug_force_sib_stride(257) == N._lib.NICE_ERR_INVALID
+    # production pick restored: the same field, the model's stride
+    h, lst = ctx.detailed_raw(s, s + n, base)
+    assert _dist(h) == want.distribution and lst == want.nice_numbers
