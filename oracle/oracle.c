@@ -568,6 +568,14 @@ static int common_msd_len(const u32 *a, int na, const u32 *b, int nb) {
 
 #define MSD_LSD_K 2 /* MSD_LSD_OVERLAP_K_VALUE, msd_prefix_filter.rs:287 */
 
+/* Study switch, not part of the restatement (scripts/filter_c_share.py):
+ * 0 turns Filter C off.  Filter C judges a range by FIRST's two LSDs when
+ * first / b^2 == last / b^2 -- a condition on the high digits, under which
+ * n mod b^2 still varies across the range -- so it is sound only for ranges
+ * of one number (which return before it); "off" is the sound filter. */
+static int g_filter_c = 1;
+void oracle_set_filter_c(int on) { g_filter_c = on; }
+
 static int has_dup_msd_prefix(u128 s, u128 e, u32 base) {
     u128 first = s, last = e - 1;
     if (e - s == 1) return 0;
@@ -591,7 +599,7 @@ static int has_dup_msd_prefix(u128 s, u128 e, u32 base) {
     /* Filter C, msd_prefix_filter.rs:461-559 */
     u128 bk = 1;
     for (int i = 0; i < MSD_LSD_K; i++) bk *= base; /* saturating_pow cannot saturate here */
-    if (first / bk == last / bk) {
+    if (g_filter_c && first / bk == last / bk) {
         int nls = nss < MSD_LSD_K ? nss : MSD_LSD_K;
         int nlc = nsc < MSD_LSD_K ? nsc : MSD_LSD_K;
         const u32 *lsd_sq = dss, *lsd_cu = dsc;

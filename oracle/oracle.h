@@ -85,6 +85,8 @@ uint64_t oracle_stride_residues(uint32_t base, uint32_t k, uint64_t *modulus,
 
 /* common/src/msd_prefix_filter.rs:382-563 (has_duplicate_msd_prefix), on the
  * half-open range [start, end). */
+/* Study switch (scripts/filter_c_share.py): 0 turns Filter C off (default 1). */
+void oracle_set_filter_c(int on);
 int oracle_has_duplicate_msd_prefix(uint64_t start_lo, uint64_t start_hi,
                                     uint64_t end_lo, uint64_t end_hi, uint32_t base);
 

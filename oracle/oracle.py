@@ -58,6 +58,8 @@ def lib():
         L.oracle_lsd_bitmap.restype = ctypes.c_int64
         L.oracle_stride_residues.argtypes = [u32, u32, P64, P64, u64]
         L.oracle_stride_residues.restype = u64
+        L.oracle_set_filter_c.argtypes = [i32]
+        L.oracle_set_filter_c.restype = None
         L.oracle_has_duplicate_msd_prefix.argtypes = [u64, u64, u64, u64, u32]
         L.oracle_has_duplicate_msd_prefix.restype = i32
         L.oracle_valid_ranges.argtypes = [u64, u64, u64, u64, u32, u64, P64, u64]

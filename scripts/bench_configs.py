@@ -135,6 +135,11 @@ def main():
     # (scripts/massive_floor_sweep.py: the fastest floor on one GPU,
     # profiles/r05/massive_floor_low.log).  The nice list is floor-independent
     # and must equal the fixture's; ranges / candidates are this floor's own.
+    # Reference-quirk dependent: Filter C (msd_prefix_filter.rs:461-559) judges
+    # a range by its first number's two LSDs, which is unsound for ranges of
+    # more than one number, and it is what prunes at this floor -- 93 % of the
+    # sound filter's candidates at floor 64, 78 % at floor 250
+    # (scripts/filter_c_share.py, profiles/r06/filter_c_share.txt).
     sec, (lst, st) = timed(lambda: ctx.niceonly_raw(m.range_start, m.range_end, 50, chunk_size=10 ** 8,
                                                      msd_floor=THROUGHPUT_FLOOR, msd_where="device"), 3)
     assert [str(x) for x in lst] == [str(x) for w in fx["windows"] for x in w["nice_numbers"]], lst
@@ -142,7 +147,9 @@ def main():
                 "size": m.range_size, "numbers_per_sec": m.range_size / sec, "wall_ms": sec * 1e3,
                 "msd_floor": THROUGHPUT_FLOOR, "msd_ranges": st.ranges, "candidates": st.candidates,
                 "nice": [str(x) for x in lst], "chunk": 10 ** 8,
-                "note": "whole field, throughput MSD floor (parity row: 'massive', floor 250)"})
+                "note": "whole field, throughput MSD floor (parity row: 'massive', floor 250); "
+                        "reference-quirk dependent: Filter C (unsound for ranges of > 1 number) removes "
+                        "93 % of the sound filter's candidates at this floor (profiles/r06/filter_c_share.txt)"})
     t1f = sec * 1e3
     shares = []
     for r in range(W):
