@@ -301,7 +301,13 @@ struct Cfg {
     // t + WG/2).
     static constexpr int HQ = 2;
     static constexpr int HROW = WG / HQ;  // counters per window row
-    static constexpr int HIST_BYTES = W * HROW * 4;
+    // VD & 8192 (sibling lanes): branch-free window count -- every number's
+    // count goes to row min(uw, W), row W a dummy row that absorbs the
+    // out-of-window counts, which are recorded afterwards on one rare path per
+    // step for all siblings (walk_sib_pipe) instead of an exec-masked branch
+    // around each sibling's count.
+    static constexpr bool BFW = (VD_ & 8192) != 0 && SIB_ > 1;
+    static constexpr int HIST_BYTES = (W + (BFW ? 1 : 0)) * HROW * 4;
     // Layout.  Default: [window rows | out-of-window bins (OUTL) | tables].
     // The digit-pair table needs at least EBT below it: S limbs are stored
     // biased by EBT and looked up at (TB - EBT) + S, an unsigned immediate
@@ -442,7 +448,7 @@ struct Cfg {
     static constexpr bool VDL = (VD & 256) != 0 && !LSD;
     static constexpr u32 MAGIC_D = (u32)(((1ull << 32) + ES * BASE - 1) / (ES * BASE));
     static_assert(VD == 0 || (MW >= 2 && split_exact(BASE, ES, MAGIC_D)), "VALU digit split");
-    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1 && (VD & ~0x1fff) == 0 &&
+    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1 && (VD & ~0x3fff) == 0 &&
                       ((VD & 1024) == 0 || LSDX),
                   "VALU-decoded limbs");
     // Waves per SIMD: what the LDS allows, capped by what the lane state
@@ -1465,6 +1471,10 @@ __device__ __forceinline__ SibUnit sib_unit(const Fd2Args &a) {
 
 // Histogram / near-miss record of sibling j's number at step i (mask m).
 template <class P>
+__device__ __forceinline__ void sib_record(u32 u, int j, u32 i, const Fd2Args &a, u32 *outl, u32 cutoff,
+                                           const NumOut &out);
+
+template <class P>
 __device__ __forceinline__ void sib_count(const u32 (&m)[P::MW], int j, u32 i, const unsigned char *smem,
                                           const Fd2Args &a, u32 hbase, u32 hinc, u32 *outl, u32 cutoff,
                                           const NumOut &out) {
@@ -1474,7 +1484,16 @@ __device__ __forceinline__ void sib_count(const u32 (&m)[P::MW], int j, u32 i, c
     if (uw < (u32)P::W) {
         atomicAdd((u32 *)(smem + uw * (P::HROW * 4) + hbase), hinc);
     } else {
-        const u32 u = uw + P::W0;
+        sib_record<P>(uw + P::W0, j, i, a, outl, cutoff, out);
+    }
+}
+
+// An out-of-window count u of sibling j's number at step i: the workgroup's
+// out-of-window bin and, above the cutoff, the near-miss list.
+template <class P>
+__device__ __forceinline__ void sib_record(u32 u, int j, u32 i, const Fd2Args &a, u32 *outl, u32 cutoff,
+                                           const NumOut &out) {
+    {
         atomicAdd(&outl[u], 1u);
         if (u > cutoff) {
             const SibUnit su = sib_unit<P>(a);
@@ -1531,6 +1550,8 @@ __device__ __forceinline__ void walk_sib_pipe(State<P> (&st)[P::SIB], const unsi
         __builtin_amdgcn_sched_barrier(0);
         u32 m0[P::MW];
         bool topS[M], topC[M];
+        u32 pack = 0;      // BFW: the siblings' unique counts, 8 bits each
+        bool oow = false;  // BFW: some sibling's count is out of the window
 #pragma unroll
         for (int j = 0; j < M; j++) {
             if (j == 0) {
@@ -1543,14 +1564,40 @@ __device__ __forceinline__ void walk_sib_pipe(State<P> (&st)[P::SIB], const unsi
             sib_consume<P>(st[j], e[j], m);
             // probe 16 (wrong by design): no window count, the mask feeds a
             // register sum instead
-            if constexpr ((P::PROBE & 16) != 0) any |= (m[0] ^ m[1]) == 0x5a5a5a5au;
-            else sib_count<P>(m, j, i, smem, a, hbase, hinc, outl, cutoff, out);
+            if constexpr ((P::PROBE & 16) != 0) {
+                any |= (m[0] ^ m[1]) == 0x5a5a5a5au;
+            } else if constexpr (P::BFW) {
+                const u32 uw = bcnt_acc(m[0], (u32)(-P::W0)) + __popc(m[1]);
+                atomicAdd((u32 *)(smem + __builtin_elementwise_min(uw, (u32)P::W) * (P::HROW * 4) + hbase), hinc);
+                // probe 32 (wrong by design): out-of-window counts are not
+                // recorded (the ceiling of a branch-free count)
+                if constexpr ((P::PROBE & 32) == 0) {
+                    pack |= (uw + P::W0) << (8 * j);
+                    oow |= uw >= (u32)P::W;
+                }
+            } else {
+                sib_count<P>(m, j, i, smem, a, hbase, hinc, outl, cutoff, out);
+            }
             any |= sib_upper_step<P>(st[j], cC, cS, topS[j], topC[j]);
             if (j + 2 < M) sib_issue<P>(st[j + 2], smem, e[j + 2]);
             __builtin_amdgcn_sched_barrier(0);
         }
         // probe 8 (wrong by design): the rare path never runs
-        if ((P::PROBE & 8) == 0 && any) rare_sib<P>(st, smem, topS, topC);
+        if constexpr (P::BFW) {
+            // one branch for both rare events (the loop's back edge when neither)
+            if (any | oow) {
+                if (oow) {
+#pragma unroll
+                    for (int j = 0; j < M; j++) {
+                        const u32 u = (pack >> (8 * j)) & 0xffu;
+                        if (u - (u32)P::W0 >= (u32)P::W) sib_record<P>(u, j, i, a, outl, cutoff, out);
+                    }
+                }
+                if ((P::PROBE & 8) == 0 && any) rare_sib<P>(st, smem, topS, topC);
+            }
+        } else if ((P::PROBE & 8) == 0 && any) {
+            rare_sib<P>(st, smem, topS, topC);
+        }
     }
 }
 
