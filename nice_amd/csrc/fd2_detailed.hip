@@ -164,7 +164,7 @@ hipError_t launch_detailed_fd2(const DetailedLaunch &p, int num_cus, hipStream_t
         q.start_lo = (uint64_t)a;
         q.start_hi = (uint64_t)(a >> 64);
         q.count = (uint64_t)(stop - a);
-        q.fin = stop == e ? p.fin : FieldFinish{nullptr, nullptr};  // finish with the last launch
+        q.fin = stop == e ? p.fin : FieldFinish{nullptr, nullptr, 0, 0};  // finish with the last launch
         hipError_t err = fd2::launch_segment(q, t.combos[i], num_cus, s);
         if (err != hipSuccess) return err;
         a = stop;

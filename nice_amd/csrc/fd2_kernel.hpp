@@ -318,7 +318,13 @@ struct Cfg {
     // unsigned 16-bit immediate offsets.
     static constexpr int T2 = SPLIT ? std::max((4 * NBINS + 15) / 16 * 16, ((int)EBT / 2 + 15) / 16 * 16) : 0;
     static constexpr int TB0 = SPLIT ? (T2 + 4 * (int)B + 15) / 16 * 16 : (HIST_BYTES + 4 * NBINS + 15) / 16 * 16;
-    static constexpr int TB = TB0 >= (int)EBT ? TB0 : ((int)EBT + 15) / 16 * 16;
+    // VD & 32768 (small fields): no table image at all -- every limb decoded
+    // by VALU, limb 0 included -- so no per-workgroup table DMA (the table
+    // loads of a small field's hundreds of workgroups are fetched through the
+    // fabric: b40 1e6 spends a median 1.5 us, b80 1e6 4.6 us, of each
+    // workgroup's life on its state and tables; profiles/r06/stamps_r06.log)
+    static constexpr bool NOTAB = (VD_ & 32768) != 0;
+    static constexpr int TB = NOTAB || TB0 >= (int)EBT ? TB0 : ((int)EBT + 15) / 16 * 16;
     static constexpr int OUTL = SPLIT ? 0 : HIST_BYTES;  // per-workgroup histogram of out-of-window counts
     static constexpr int TC0 = (SPLIT ? T2 : TB) / 16 * 16;  // the table image starts here (16-byte copy)
     // Low-digit entry, word 1: digit bits [0, DB), then the carries and flags
@@ -332,7 +338,9 @@ struct Cfg {
     // extra multiply-add per step); wider bases have no low-digit table.
     static constexpr int DB = BASE - 32;
     static constexpr bool TIGHT = DB > 20;
-    static constexpr bool LSD_W1 = MW == 2 && DB > 0 && DB + (TIGHT ? 4 : 10) <= 30;
+    // VD & 16384 (small fields): no low-digit table, limb 0 stepped like the
+    // others (a 12.8 KB instead of a 38.4 KB table image at b40)
+    static constexpr bool LSD_W1 = MW == 2 && DB > 0 && DB + (TIGHT ? 4 : 10) <= 30 && (VD_ & (16384 | 32768)) == 0;
     // VD & 1024 (probe A/B, b59..64: word 1 of the entry is all digit bits):
     // the low-digit table with the carries and wrap flags in a side table of
     // bytes (bit 0 the S carry, bits 1-3 the C carry, bit 6 / 7 the D1 / N3
@@ -341,7 +349,7 @@ struct Cfg {
     static constexpr bool LSDX = MW == 2 && DB > 0 && !LSD_W1 && (VD_ & 1024) != 0;
     static constexpr bool LSD = LSD_W1 || LSDX;
     // (regions padded to 16 bytes: the image is copied in with 16-byte accesses)
-    static constexpr int TL = TB + ((int)(B * ES) + 15) / 16 * 16;  // low-digit table (LDE entries)
+    static constexpr int TL = TB + (NOTAB ? 0 : ((int)(B * ES) + 15) / 16 * 16);  // low-digit table (LDE entries)
     // Low-digit entries: a lane whose chunk starts at n reads n mod B + i, i <
     // chunk <= B, so 2B cover any chunk.  The sibling kernels of b46+ keep
     // B + 256 (their chunks are capped at 256, launch_sib): the table then
@@ -399,9 +407,11 @@ struct Cfg {
     // lookups bank-conflict the most (sibling lanes, which have VALU to spare)
     static constexpr bool VDLOW = (VD & 4096) != 0;
     static constexpr bool vd_s(int q) {
+        if (NOTAB) return true;
         return VDLOW ? (q > LO && q <= LO + VDS && q < SL) : (q >= SL - VDB - VDS && q < SL - VDB);
     }
     static constexpr bool vd_c(int q) {
+        if (NOTAB) return true;
         return VDLOW ? (q > LO && q <= LO + VDC && q < CL) : (q >= CL - VDB - VDC && q < CL - VDB);
     }
     // Lookup groups: a scheduling barrier after every LG table lookups of a
@@ -445,16 +455,20 @@ struct Cfg {
     // VD & 256 (no low-digit table only): limb 0 of S and of C by VALU too --
     // n^2 mod B and n^3 mod B of a wave's lanes keep few residues mod 16, so
     // their lookups pile onto few bank quads
-    static constexpr bool VDL = (VD & 256) != 0 && !LSD;
+    static constexpr bool VDL = ((VD & 256) != 0 || NOTAB) && !LSD;
     static constexpr u32 MAGIC_D = (u32)(((1ull << 32) + ES * BASE - 1) / (ES * BASE));
     static_assert(VD == 0 || (MW >= 2 && split_exact(BASE, ES, MAGIC_D)), "VALU digit split");
-    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1 && (VD & ~0x3fff) == 0 &&
+    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1 && (VD & ~0xffff) == 0 &&
                       ((VD & 1024) == 0 || LSDX),
                   "VALU-decoded limbs");
     // Waves per SIMD: what the LDS allows, capped by what the lane state
     // needs in VGPRs (the register budget is set to match, see state_waves).
     static constexpr int WPE0 = (163840 / LDS_BYTES) * (WG / 64) / 4;
-    static constexpr int WPE1 = WPE0 < sib_waves(BASE, SIB) ? WPE0 : sib_waves(BASE, SIB);
+    // (the small-field variants -- no low-digit table / no table -- at a
+    // 128-VGPR budget: a field below 1e7 puts only a few waves on each SIMD)
+    // (three mask words without a table: 256 VGPRs)
+    static constexpr int WREG = (VD_ & 32768) && MW == 3 ? 2 : (VD_ & (16384 | 32768)) ? 4 : sib_waves(BASE, SIB);
+    static constexpr int WPE1 = WPE0 < WREG ? WPE0 : WREG;
     // in whole workgroups: k = the workgroups a CU holds at WPE1 waves per
     // SIMD (a workgroup's WG / 64 waves spread over the 4 SIMDs), then the
     // waves per SIMD those k workgroups need (640-thread workgroups: 2.5 each)
@@ -464,7 +478,9 @@ struct Cfg {
     static_assert(SL < NS && CL < NC && EL <= NE, "FD layout needs cached high limbs");
     static_assert(ND <= NX + 1 && NE2 <= NX + 1 && NE <= NS + 1, "difference limb counts");
     static_assert(S_TOPD >= 1 && C_TOPD >= 1, "top limb");
-    static_assert(TB >= (int)EBT && TB - (int)EBT < 65536 && (!LSD || LSDX || TL < 65536), "LDS offsets");
+    static_assert((NOTAB || TB >= (int)EBT) && (NOTAB || TB - (int)EBT < 65536) && (!LSD || LSDX || TL < 65536),
+                  "LDS offsets");
+    static_assert(!NOTAB || (!LSD && !SPLIT && SIB_ == 1), "table-free kernel: regular lanes, no low-digit table");
     static_assert(!SPLIT || (T2 >= (int)EBT / 2 && T2 < 65536 && T2 + 4 * (int)B <= TB && 4 * NBINS <= TC0 &&
                              ES == 8 && TB < 65536),
                   "split layout");
@@ -586,7 +602,8 @@ __device__ __forceinline__ void or_valu(u32 vs, u32 (&m)[P::MW]) {
 template <class P>
 __device__ __forceinline__ void or_plain(const unsigned char *smem, u32 v, int digits, u32 (&m)[P::MW]) {
     if (digits == 2) {
-        or_lookup<P, P::TB, P::T2>(smem, v * P::ES, m);
+        if constexpr (P::NOTAB) or_valu<P>(v * P::ES, m);
+        else or_lookup<P, P::TB, P::T2>(smem, v * P::ES, m);
     } else {
 #pragma unroll
         for (int w = 0; w < P::MW; w++) m[w] |= (v >> 5) == (u32)w ? 1u << (v & 31) : 0u;
@@ -944,6 +961,11 @@ __global__ void fd2_tables_kernel(unsigned char *tb) {
 // depends on the base only) and kept for the process.
 template <class P>
 static hipError_t fd2_tables(hipStream_t s, const uint4 **out) {
+    if constexpr (P::TAB_BYTES == 0) {  // table-free kernel (Cfg::NOTAB)
+        (void)s;
+        *out = nullptr;
+        return hipSuccess;
+    }
     static std::mutex mu;
     static std::map<int, unsigned char *> have;
     int dev = 0;
@@ -1026,7 +1048,7 @@ struct Fd2Args {
 // here would write back and invalidate the XCD's whole L2 once per
 // workgroup: 12 000 of them made the b40 1e9 field 1.8x slower.
 template <int WG>
-__device__ __forceinline__ void field_finish(const FieldFinish &fin, u64 *hist, u32 ncopies, u32 *count,
+__device__ __forceinline__ void field_finish(const FieldFinish &fin, u64 *hist, u32 ncopies, u32 nbins, u32 *count,
                                              unsigned char *smem, u64 *stamps) {
     (void)stamps;
     __shared__ u32 last;
@@ -1040,32 +1062,50 @@ __device__ __forceinline__ void field_finish(const FieldFinish &fin, u64 *hist, 
     for (u32 b = threadIdx.x; b < 129; b += WG) acc[b] = 0;
     __syncthreads();
     // All of a lane's loads issued before the first is used: one L2 round
-    // trip for the ncopies x 129 copies instead of one per copy row.
+    // trip for the copies instead of one per copy row.  Only bins < nbins
+    // (base + 1) are read: the field's launches touch no other bin, and every
+    // finish leaves the bins it read at zero (the generic kernel's finish
+    // kernel zeroes all of them).
     constexpr u32 PER = (kHistCopies * 129 + WG - 1) / WG;
-    const u32 NE = ncopies * 129;
+    const u32 NE = ncopies * nbins;
     const u32 nmiss = threadIdx.x == 0 ? __hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
     u64 v[PER];
+    u32 at[PER];
 #pragma unroll
     for (u32 k = 0; k < PER; k++) {
         const u32 e = threadIdx.x + k * WG;
-        v[k] = e < NE ? __hip_atomic_load(&hist[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        const u32 c = e / nbins, b = e - c * nbins;
+        at[k] = c * 129 + b;
+        v[k] = e < NE ? __hip_atomic_load(&hist[at[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
     }
 #pragma unroll
     for (u32 k = 0; k < PER; k++) {
-        const u32 e = threadIdx.x + k * WG;
         if (v[k]) {
-            atomicAdd(&acc[e % 129], (unsigned long long)v[k]);
-            __hip_atomic_store(&hist[e], (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            atomicAdd(&acc[at[k] % 129], (unsigned long long)v[k]);
+            __hip_atomic_store(&hist[at[k]], (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __syncthreads();
     FD2_STAMP_P(stamps, 8);  // copies read and summed
+    done_reset(fin.done);
+    if (fin.tag) {
+        // tagged words (FieldFinish::tag): no store-completion wait, no
+        // sequence word; the kernel's end orders the re-zeroing for the slot's
+        // next field
+        const u64 t = (u64)fin.tag << 32;
+        for (u32 b = threadIdx.x; b < nbins; b += WG) fin.out_mapped[b] = t | (u32)acc[b];
+        if (threadIdx.x == 0) {
+            fin.out_mapped[129] = t | nmiss;
+            __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        FD2_STAMP_P(stamps, 9);
+        return;
+    }
     for (u32 b = threadIdx.x; b < 129; b += WG) fin.out_mapped[b] = acc[b];
     if (threadIdx.x == 0) {
         fin.out_mapped[129] = nmiss;
         __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    done_reset(fin.done);
     // Publish: every lane's mapped stores complete, then one system-scope
     // release store of the sequence number (once per field, so its L2
     // write-back costs nothing measurable).
@@ -1868,7 +1908,7 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
     FD2_STAMP(a, 5);  // histogram flushed (thread 0's part)
     if (a.fin.out_mapped) {
         __syncthreads();  // smem is reused by the finish
-        field_finish<P::WG>(a.fin, a.hist, a.ncopies, out.count, smem, a.stamps);
+        field_finish<P::WG>(a.fin, a.hist, a.ncopies, P::NBINS, out.count, smem, a.stamps);
     }
     FD2_STAMP(a, 6);  // end (the finishing workgroup: after the finish)
 }
@@ -2162,7 +2202,7 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         a.out = q.out;
         a.tabs = tabs;
         // the field's finish rides on its last launch
-        a.fin = left == cnt ? q.fin : FieldFinish{nullptr, nullptr};
+        a.fin = left == cnt ? q.fin : FieldFinish{nullptr, nullptr, 0, 0};
         NICE_PROBE_ONLY({
             const u64 v[6] = {grid, (u64)P::WG, chunk, nunits, tail, (u64)per_cu};
             for (int k = 0; k < 6; k++) g_last_launch[k] = v[k];
@@ -2300,7 +2340,7 @@ static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s
         a.hist = q.hist;
         a.out = q.out;
         a.tabs = tabs;
-        a.fin = left == cnt ? q.fin : FieldFinish{nullptr, nullptr};
+        a.fin = left == cnt ? q.fin : FieldFinish{nullptr, nullptr, 0, 0};
         const u64 grid = (u64)a.sib_blocks + a.edge_blocks + a.main_blocks + (tail + P::WG - 1) / P::WG;
         NICE_PROBE_ONLY({
             const u64 v[6] = {grid, (u64)P::WG, L, Q * upb, R, (u64)per_cu};

@@ -29,6 +29,12 @@ struct FieldFinish {
     uint64_t *out_mapped;
     uint32_t *done;  // kDoneWords arrival counters (nice_device.hpp), re-zeroed by the finish
     uint64_t seq;    // the field's sequence number (nonzero)
+    // Nonzero (fields of < 2^31 numbers): every result word is published as
+    // tag << 32 | value -- bins 0..base and the near-miss count [129] -- with
+    // no ordering among them and no sequence word; the host takes the field
+    // as finished once every word carries the tag (one fewer round trip to
+    // host memory than stores, wait, release store of the sequence word).
+    uint32_t tag;
 };
 
 struct DetailedLaunch {

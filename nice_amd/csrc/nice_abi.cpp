@@ -151,6 +151,8 @@ struct Slot {
     uint32_t launches = 0;        // ... and its kernel launches (the finish kernel not counted)
     uint32_t sib[2] = {0, 0};     // ... and its last sibling-lane launch: lanes M, stride L
     bool fin_seq = false;         // ... and whether its fd2 finish publishes it
+    uint32_t tag = 0;             // ... as tagged words (FieldFinish::tag; 0: bins + sequence word)
+    uint32_t tag_words = 0;       // ... bins 0..tag_words-1 (and [129]) carry the tag
     MsdBuf msd;
 };
 
@@ -521,6 +523,9 @@ int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *f
     p.launches = &sl.launches;
     p.sib = sl.sib;
     *finished = false;
+    // Small fields run wholly by fd2 publish tagged result words
+    // (FieldFinish::tag): one fewer round trip to host memory at their end.
+    uint32_t tag = 0;
     auto launch = [&](u128 a, u128 b, bool fd) -> int {
         if (a >= b) return NICE_OK;
         u128 cnt = b - a;
@@ -531,16 +536,20 @@ int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *f
             p.count = c;
             // the field's last launch finishes it when it is an fd2 launch
             const bool last = a + c == e;
-            p.fin = last && fd ? nice::FieldFinish{sl.d_fin, sl.d_done, sl.seq}
-                               : nice::FieldFinish{nullptr, nullptr, 0};
-            if (nice::probe_set("NICE_FD2_NOFIN")) p.fin = nice::FieldFinish{nullptr, nullptr, 0};  // probe: finish kernel
+            p.fin = last && fd ? nice::FieldFinish{sl.d_fin, sl.d_done, sl.seq, tag}
+                               : nice::FieldFinish{nullptr, nullptr, 0, 0};
+            if (nice::probe_set("NICE_FD2_NOFIN")) p.fin = nice::FieldFinish{nullptr, nullptr, 0, 0};  // probe: finish kernel
             const bool fd2 = fd;
             hipError_t err = fd ? nice::launch_detailed_fd2(p, d.num_cus, sl.stream)
                                 : nice::launch_detailed_generic(p, d.num_cus, sl.stream);
             if (!fd) sl.launches++;
             if (err != hipSuccess)
                 return fail(NICE_ERR_HIP, std::string("detailed launch: ") + hipGetErrorString(err));
-            if (last) *finished = fd2 && p.fin.out_mapped;
+            if (last) {
+                *finished = fd2 && p.fin.out_mapped;
+                sl.tag = *finished ? p.fin.tag : 0u;
+                sl.tag_words = base + 1;
+            }
             a += c;
             cnt -= c;
         }
@@ -553,7 +562,11 @@ int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *f
     // wholly by fd2 keeps 16 (its whole grid flushes at once, and the
     // in-kernel finish reads every copy in use); anything else all 64 (the
     // generic kernel and the finish kernel use all of them).
-    p.hist_copies = fd && s >= rs && e <= re && e - s < 20000000 ? 16 : nice::kHistCopies;
+    const bool small_fd = fd && s >= rs && e <= re && e - s < 20000000;
+    p.hist_copies = small_fd ? 16 : nice::kHistCopies;
+    // (probe: NICE_FD2_UNTAGGED publishes bins + sequence word as large fields do)
+    if (small_fd && !nice::probe_set("NICE_FD2_UNTAGGED")) tag = (uint32_t)sl.seq | 0x80000000u;
+    sl.tag = 0;
     if (!fd) return launch(s, e, false);
     int rc;
     if ((rc = launch(s, std::min(e, rs), false))) return rc;
@@ -637,6 +650,16 @@ int resolve_stats(Device &d) {
 // completion signal (which still follows: the last workgroup retires after
 // publishing).  The completion event is queried every 4096 polls, so a failed
 // launch or a finish that never publishes is reported, not spun on.
+// A field's published result words: its sequence word, or (tagged fields)
+// every bin word and the near-miss count carrying the field's tag.
+bool published(const Slot &sl) {
+    if (!sl.tag) return __atomic_load_n(&sl.h_fin[130], __ATOMIC_ACQUIRE) == sl.seq;
+    if ((uint32_t)(__atomic_load_n(&sl.h_fin[129], __ATOMIC_ACQUIRE) >> 32) != sl.tag) return false;
+    for (uint32_t b = 0; b < sl.tag_words; b++)
+        if ((uint32_t)(__atomic_load_n(&sl.h_fin[b], __ATOMIC_ACQUIRE) >> 32) != sl.tag) return false;
+    return true;
+}
+
 int wait_field(Slot &sl) {
     if (!sl.fin_seq || !spin_wait()) {
         const hipError_t q = field_sync(sl);
@@ -644,11 +667,11 @@ int wait_field(Slot &sl) {
         return NICE_OK;
     }
     for (uint32_t i = 1;; i++) {
-        if (__atomic_load_n(&sl.h_fin[130], __ATOMIC_ACQUIRE) == sl.seq) return NICE_OK;
+        if (published(sl)) return NICE_OK;
         if ((i & 4095) == 0 || i > kSpinPolls) {
             const hipError_t q = field_query(sl);
             if (q == hipSuccess) {
-                if (__atomic_load_n(&sl.h_fin[130], __ATOMIC_ACQUIRE) == sl.seq) return NICE_OK;
+                if (published(sl)) return NICE_OK;
                 return fail(NICE_ERR_HIP, "detailed field completed without publishing its results");
             }
             if (q != hipErrorNotReady) return fail(NICE_ERR_HIP, std::string("detailed field: ") + hipGetErrorString(q));
@@ -761,7 +784,7 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
             cnt = (uint32_t)sl.h_fin[129];
             if (cnt > sl.det.cap) return fail(NICE_ERR_HIP, "near-miss list overflow after resize");
         }
-        for (uint32_t b = 0; b <= base; b++) job.total[b] += sl.h_fin[b];
+        for (uint32_t b = 0; b <= base; b++) job.total[b] += sl.tag ? (uint32_t)sl.h_fin[b] : sl.h_fin[b];
         if (cnt) {
             // the list is read after the kernel has retired (its end-of-kernel
             // cache write-back), not merely published its count

@@ -64,7 +64,7 @@ static double run(u64 start, u64 count, std::vector<u64> &hist, u32 &nmiss, int 
         p.hist = d_hist;
         p.hist_copies = kHistCopies;
         p.out = NumOut{d_n, d_u, d_count, 1u << 20};
-        p.fin = FieldFinish{nullptr, nullptr, 0};
+        p.fin = FieldFinish{nullptr, nullptr, 0, 0};
         hipEventRecord(e0, 0);
         hipError_t e = launch_cfg<P>(p, cus, 0);
         hipEventRecord(e1, 0);
