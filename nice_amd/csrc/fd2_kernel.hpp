@@ -301,13 +301,12 @@ struct Cfg {
     // t + WG/2).
     static constexpr int HQ = 2;
     static constexpr int HROW = WG / HQ;  // counters per window row
-    // VD & 8192 (sibling lanes): branch-free window count -- every number's
-    // count goes to row min(uw, W), row W a dummy row that absorbs the
-    // out-of-window counts, which are recorded afterwards on one rare path per
-    // step for all siblings (walk_sib_pipe) instead of an exec-masked branch
-    // around each sibling's count.
-    static constexpr bool BFW = (VD_ & 8192) != 0 && SIB_ > 1;
-    static constexpr int HIST_BYTES = (W + (BFW ? 1 : 0)) * HROW * 4;
+    // (A branch-free window count -- every count to row min(uw, W), a dummy
+    // row W, out-of-window counts recorded behind one wave-uniform branch --
+    // measured 1 % slower on the b40 sibling kernel; skipping the
+    // out-of-window work altogether, wrong by design, only 3 % faster:
+    // profiles/r06/occupancy_ab.txt, bfw_uniform_branch_ab.log.)
+    static constexpr int HIST_BYTES = W * HROW * 4;
     // Layout.  Default: [window rows | out-of-window bins (OUTL) | tables].
     // The digit-pair table needs at least EBT below it: S limbs are stored
     // biased by EBT and looked up at (TB - EBT) + S, an unsigned immediate
@@ -1590,8 +1589,6 @@ __device__ __forceinline__ void walk_sib_pipe(State<P> (&st)[P::SIB], const unsi
         __builtin_amdgcn_sched_barrier(0);
         u32 m0[P::MW];
         bool topS[M], topC[M];
-        u32 pack = 0;      // BFW: the siblings' unique counts, 8 bits each
-        bool oow = false;  // BFW: some sibling's count is out of the window
 #pragma unroll
         for (int j = 0; j < M; j++) {
             if (j == 0) {
@@ -1606,15 +1603,6 @@ __device__ __forceinline__ void walk_sib_pipe(State<P> (&st)[P::SIB], const unsi
             // register sum instead
             if constexpr ((P::PROBE & 16) != 0) {
                 any |= (m[0] ^ m[1]) == 0x5a5a5a5au;
-            } else if constexpr (P::BFW) {
-                const u32 uw = bcnt_acc(m[0], (u32)(-P::W0)) + __popc(m[1]);
-                atomicAdd((u32 *)(smem + __builtin_elementwise_min(uw, (u32)P::W) * (P::HROW * 4) + hbase), hinc);
-                // probe 32 (wrong by design): out-of-window counts are not
-                // recorded (the ceiling of a branch-free count)
-                if constexpr ((P::PROBE & 32) == 0) {
-                    pack |= (uw + P::W0) << (8 * j);
-                    oow |= uw >= (u32)P::W;
-                }
             } else {
                 sib_count<P>(m, j, i, smem, a, hbase, hinc, outl, cutoff, out);
             }
@@ -1623,21 +1611,7 @@ __device__ __forceinline__ void walk_sib_pipe(State<P> (&st)[P::SIB], const unsi
             __builtin_amdgcn_sched_barrier(0);
         }
         // probe 8 (wrong by design): the rare path never runs
-        if constexpr (P::BFW) {
-            // one branch for both rare events (the loop's back edge when neither)
-            if (any | oow) {
-                if (oow) {
-#pragma unroll
-                    for (int j = 0; j < M; j++) {
-                        const u32 u = (pack >> (8 * j)) & 0xffu;
-                        if (u - (u32)P::W0 >= (u32)P::W) sib_record<P>(u, j, i, a, outl, cutoff, out);
-                    }
-                }
-                if ((P::PROBE & 8) == 0 && any) rare_sib<P>(st, smem, topS, topC);
-            }
-        } else if ((P::PROBE & 8) == 0 && any) {
-            rare_sib<P>(st, smem, topS, topC);
-        }
+        if ((P::PROBE & 8) == 0 && any) rare_sib<P>(st, smem, topS, topC);
     }
 }
 
