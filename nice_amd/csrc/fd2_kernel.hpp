@@ -268,6 +268,15 @@ struct Cfg {
     static constexpr int D3 = r5 == 0 ? 3 * k : (r5 == 2 ? 3 * k + 1 : 3 * k + 2);
     static constexpr int DN = r5 == 0 ? k : k + 1;
     static constexpr bool N64 = fits64(BASE, DN);  // init's u64 path
+    // init's products in u64 columns (the 1024-thread kernels of the bases
+    // whose n passes 64 bits: the register allocation that spills least);
+    // elsewhere u32 columns (every FD base's column sums fit 32 bits:
+    // static_assert below), normalised by 32-bit multiply-highs
+    // VD & 65536 (probe A/B): the round-5 init -- init_digits on the 128-bit n
+    // and u64 columns -- also on the 512-thread kernels of the bases whose n
+    // passes 64 bits
+    static constexpr bool OLDINIT = (VD_ & 65536) != 0;
+    static constexpr bool C64 = !N64 && (WG_ >= 1024 || OLDINIT);
     static constexpr int NS = cdiv(D2, 2), NC = cdiv(D3, 2), NX = cdiv(DN, 2);
     static constexpr int SL = ND + 1, CL = NE + 1, EL = NE2 + 1;  // per-step limbs
     static constexpr int S_TOPD = D2 - 2 * (NS - 1), C_TOPD = D3 - 2 * (NC - 1);
@@ -457,7 +466,7 @@ struct Cfg {
     static constexpr bool VDL = ((VD & 256) != 0 || NOTAB) && !LSD;
     static constexpr u32 MAGIC_D = (u32)(((1ull << 32) + ES * BASE - 1) / (ES * BASE));
     static_assert(VD == 0 || (MW >= 2 && split_exact(BASE, ES, MAGIC_D)), "VALU digit split");
-    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1 && (VD & ~0xffff) == 0 &&
+    static_assert(VDC <= NE + 1 - (MW <= 2 ? 1 : 0) && VDS <= ND + 1 && (VD & ~0x1ffff) == 0 &&
                       ((VD & 1024) == 0 || LSDX),
                   "VALU-decoded limbs");
     // Waves per SIMD: what the LDS allows, capped by what the lane state
@@ -687,7 +696,7 @@ __device__ __forceinline__ void init_plain(State<P> &st, const u32 (&X)[P::NX]) 
     // Column sums: at most min(NS, NX) products < B^2 plus a carry: 32 bits
     // (Cfg static_assert).
     using A = u32;
-    if constexpr (!P::N64) {
+    if constexpr (P::C64) {
         // wide bases (b80: the 1024-thread kernel at the 128-VGPR cap): u64
         // columns, the layout whose register allocation spills least.
         st.r8 = X[0] * P::ES + (P::LSDX ? (u32)P::TL : 0u);
@@ -785,6 +794,49 @@ __device__ __forceinline__ void init(State<P> &st, u64 n_lo, u64 n_hi) {
     init_digits<P>(X, n_lo, n_hi);
     init_plain<P>(st, X);
     init_scale<P>(st);
+}
+
+// Radix-B digits of n = base + off from the host's digits of the launch part's
+// first n (Fd2Args::xs / xt) and the lane's offset off < B^4: one u64
+// division by B^2 and two u32 splits, then a carried add -- instead of the
+// 128-bit n's NX x 4 u64 divisions by B (init_digits on the bases whose n
+// passes 64 bits, where the radix conversion was most of a lane's init).
+template <class P>
+__device__ __forceinline__ void digits_plus(u32 (&X)[P::NX], const u32 *xb, u64 off) {
+    constexpr u32 B = P::B;
+    constexpr u64 B2 = (u64)B * B;
+    const u64 q = off / B2;
+    const u32 r = (u32)(off - q * B2), qq = (u32)q;
+    const u32 o[4] = {r % B, r / B, qq % B, qq / B};
+    u32 c = 0;
+#pragma unroll
+    for (int i = 0; i < P::NX; i++) {
+        const u32 t = xb[i] + (i < 4 ? o[i] : 0u) + c;
+        c = t >= B ? 1u : 0u;
+        X[i] = t - c * B;
+    }
+}
+
+// init at base + off (base: the launch part whose digits the host passed).
+// Bases whose in-range n fits 64 bits keep init(): their conversion is two
+// u64 divisions.  So do the 1024-thread kernels (u64 columns): there the
+// digits path measured 1.3 % slower on b80 1e9 (6.29 vs 6.21 ms), while the
+// 512-thread small-field kernel gained 3.5 % on b80 1e6 (19.2 vs 19.9 us in
+// the A/B harness; profiles/r06/init_ab_b80.log).
+template <class P>
+__device__ __forceinline__ void init_at(State<P> &st, const u32 *xb, u64 off, u64 n_lo, u64 n_hi) {
+    if constexpr (P::N64 || P::C64) {
+        (void)xb;
+        (void)off;
+        init<P>(st, n_lo, n_hi);
+    } else {
+        (void)n_lo;
+        (void)n_hi;
+        u32 X[P::NX];
+        digits_plus<P>(X, xb, off);
+        init_plain<P>(st, X);
+        init_scale<P>(st);
+    }
 }
 
 // +ES into scaled plain limbs [from, N) (rare path).
@@ -1032,6 +1084,9 @@ struct Fd2Args {
     u64 sib_lo, sib_hi, edge_lo, edge_hi;
     u32 sib_chunk, sib_upb, sib_units, sib_blocks;
     u32 edge_chunk, edge_units, edge_blocks;
+    // radix-B digits of start (xs) and tail (xt), least significant first,
+    // for init_at (bases whose n passes 64 bits; kXDigits >= NX)
+    u32 xs[12], xt[12];
     u64 *hist;          // kHistCopies x 129 bins
     NumOut out;
     const uint4 *tabs;
@@ -1682,22 +1737,25 @@ __device__ __forceinline__ void walk_sib(State<P> (&st)[P::SIB], const unsigned 
 // unit: b < mb: main unit 64 b + lane (chunk a.chunk from a.start); else the
 // tail numbers 64 (b - mb) + lane (chunk 1 from a.tail).
 __device__ __forceinline__ void pers_unit(const Fd2Args &a, u32 b, u32 mb, u32 lane, bool &active, u64 &lo,
-                                          u64 &hi, u32 &chunk) {
+                                          u64 &hi, u32 &chunk, u64 &off, bool &tailp) {
     if (b < mb) {
         const u32 unit = 64 * b + lane;
         active = unit < a.nunits;
         lo = a.start_lo;
         hi = a.start_hi;
-        add_u128(lo, hi, (u64)unit * a.chunk);
+        off = (u64)unit * a.chunk;
+        tailp = false;
         chunk = a.chunk;
     } else {
         const u32 idx = 64 * (b - mb) + lane;
         active = idx < a.tail_count;
         lo = a.tail_lo;
         hi = a.tail_hi;
-        add_u128(lo, hi, (u64)idx);
+        off = idx;
+        tailp = true;
         chunk = 1;
     }
+    add_u128(lo, hi, off);
 }
 
 template <class P>
@@ -1760,16 +1818,19 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
     // next k to hand out
     __shared__ u32 pers_next;
     u32 pmb = 0, pnk = 0, pk = 0;
+    u64 n0_off = 0;          // n0 - the part's first n (init_at)
+    bool n0_tail = !main_part;
     if constexpr (P::PERS) {
         pmb = (a.nunits + 63) / 64;
         const u32 nb = pmb + (a.tail_count + 63) / 64, G = gridDim.x;
         pnk = nb > blockIdx.x ? (nb - blockIdx.x + G - 1) / G : 0;
         pk = tid >> 6;
         if (tid == 0) pers_next = P::WG / 64;
-        if (pk < pnk) pers_unit(a, blockIdx.x + G * pk, pmb, lane_id, active, n0_lo, n0_hi, chunk_l);
+        if (pk < pnk) pers_unit(a, blockIdx.x + G * pk, pmb, lane_id, active, n0_lo, n0_hi, chunk_l, n0_off, n0_tail);
         else active = false;
     } else {
-        add_u128(n0_lo, n0_hi, (u64)unit * chunk);
+        n0_off = (u64)unit * chunk;
+        add_u128(n0_lo, n0_hi, n0_off);
     }
     // Window counters: row u - W0, column tid mod HROW (u16 halves / u8 quarters).
     const u32 hbase = P::HB + tid % P::HROW * 4;
@@ -1804,7 +1865,7 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
         }
     }
     State<P> st;
-    if (!sib_done && active) init<P>(st, n0_lo, n0_hi);
+    if (!sib_done && active) init_at<P>(st, n0_tail ? a.xt : a.xs, n0_off, n0_lo, n0_hi);
     // The table DMA must have landed before any wave reads LDS: wait for it
     // explicitly (a workgroup barrier alone need not imply vmcnt(0)), then
     // the barrier.
@@ -1833,8 +1894,10 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
         u32 ch = chunk_l;
         while (k < pnk) {
             if (taken) {
-                pers_unit(a, blockIdx.x + gridDim.x * k, pmb, lane_id, act, m_lo, m_hi, ch);
-                if (act) init<P>(st, m_lo, m_hi);
+                u64 off = 0;
+                bool tp = false;
+                pers_unit(a, blockIdx.x + gridDim.x * k, pmb, lane_id, act, m_lo, m_hi, ch, off, tp);
+                if (act) init_at<P>(st, tp ? a.xt : a.xs, off, m_lo, m_hi);
             }
             if (act) walk_chunk<P>(st, smem, ch, m_lo, m_hi, hbase, hinc, outl, cutoff, out, probe_acc);
             if (++taken >= a.wave_cap) break;
@@ -1895,6 +1958,14 @@ fd2_kernel(Fd2Args a) {
 
 template <class P>
 static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s);
+
+// Radix-B digits of n, least significant first (Fd2Args::xs / xt).
+static inline void host_digits(u128 n, u32 B, u32 *out, int nx) {
+    for (int i = 0; i < nx; i++) {
+        out[i] = (u32)(n % B);
+        n /= B;
+    }
+}
 
 // ---------------------------------------------------------------------------
 // Lane stride from a bank-conflict model.  A wave's lanes sit `L` numbers
@@ -2169,6 +2240,10 @@ static hipError_t launch_cfg(const DetailedLaunch &p, int num_cus, hipStream_t s
         a.chunk = (u32)chunk;
         a.tail_count = (u32)tail;
         a.main_blocks = (u32)main_blocks;
+        if constexpr (!P::N64 && !P::C64) {
+            host_digits(((u128)a.start_hi << 64) | a.start_lo, P::B, a.xs, P::NX);
+            host_digits(((u128)a.tail_hi << 64) | a.tail_lo, P::B, a.xt, P::NX);
+        }
         a.cutoff = q.cutoff;
         a.ncopies = q.hist_copies;
         a.wave_cap = (u32)(65535 / chunk);

@@ -31,14 +31,23 @@ std::atomic<uint32_t> nice::fd2::g_force_sib_stride{0};  // (defined by fd2_deta
 // kernel); 1: the round-5 production b40 sibling kernel
 #if defined(XREF) && XREF == 1
 using Ref = Cfg<40, 4, 8, 5, 0, 512, 4097, 100, 0, 3>;
-#else
+#elif !defined(XREFVD)
 #define XREF 0
 using Ref = Cfg<XB, XND, XNE, XNE2, 0, big_wg(XB), valu_limbs_big(XB, XND, XNE)>;
 #endif
-using Var = Cfg<XB, XND, XNE, XNE2, XPROBE, XWG, XVD, XLG, 0, XM>;
+#ifndef XPERS
+#define XPERS 0
+#endif
+// XREFVD: the reference is the variant's own configuration at VD = XREFVD
+#ifdef XREFVD
+#undef XREF
+#define XREF 2
+using Ref = Cfg<XB, XND, XNE, XNE2, 0, XWG, XREFVD, XLG, XPERS, XM>;
+#endif
+using Var = Cfg<XB, XND, XNE, XNE2, XPROBE, XWG, XVD, XLG, XPERS, XM>;
 
 template <class P>
-static double run(u64 start, u64 count, std::vector<u64> &hist, u32 &nmiss, int reps) {
+static double run(unsigned __int128 start, u64 count, std::vector<u64> &hist, u32 &nmiss, int reps) {
     u64 *d_hist;
     u32 *d_count;
     u64 *d_n;
@@ -57,7 +66,8 @@ static double run(u64 start, u64 count, std::vector<u64> &hist, u32 &nmiss, int 
         hipMemset(d_hist, 0, kHistCopies * 129 * 8);
         hipMemset(d_count, 0, 4);
         DetailedLaunch p{};
-        p.start_lo = start;
+        p.start_lo = (u64)start;
+        p.start_hi = (u64)(start >> 64);
         p.count = count;
         p.base = XB;
         p.cutoff = (u32)(XB * 9 / 10);  // floor(b * 0.9) (number_stats.rs:15-17; exact for these bases)
@@ -90,7 +100,12 @@ static double run(u64 start, u64 count, std::vector<u64> &hist, u32 &nmiss, int 
 }
 
 int main(int argc, char **argv) {
-    const u64 start = argc > 1 ? strtoull(argv[1], 0, 10) : 1916284264916ull;
+    // START in decimal, up to 128 bits (b80 fields start above 2^64)
+    unsigned __int128 start = 1916284264916ull;
+    if (argc > 1) {
+        start = 0;
+        for (const char *c = argv[1]; *c; c++) start = start * 10 + (unsigned)(*c - '0');
+    }
     const u64 count = argc > 2 ? strtoull(argv[2], 0, 10) : 100000000ull;
     const int reps = argc > 3 ? atoi(argv[3]) : 3;
     std::vector<u64> h0, h1;
