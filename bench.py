@@ -99,7 +99,7 @@ def parse():
     return p.parse_args()
 
 
-PMC_BENCH_FILE = "profiles/r05/pmc_bench.json"
+PMC_BENCH_FILE = "profiles/r06/pmc_bench.json"
 
 
 def lib_sha16() -> str:

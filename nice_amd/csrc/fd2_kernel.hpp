@@ -489,6 +489,7 @@ struct Cfg {
     static_assert((NOTAB || TB >= (int)EBT) && (NOTAB || TB - (int)EBT < 65536) && (!LSD || LSDX || TL < 65536),
                   "LDS offsets");
     static_assert(!NOTAB || (!LSD && !SPLIT && SIB_ == 1), "table-free kernel: regular lanes, no low-digit table");
+    static_assert(!PERS || N64 || C64, "persistent grid: init() only (init_at is the rounds path's)");
     static_assert(!SPLIT || (T2 >= (int)EBT / 2 && T2 < 65536 && T2 + 4 * (int)B <= TB && 4 * NBINS <= TC0 &&
                              ES == 8 && TB < 65536),
                   "split layout");
@@ -1737,25 +1738,22 @@ __device__ __forceinline__ void walk_sib(State<P> (&st)[P::SIB], const unsigned 
 // unit: b < mb: main unit 64 b + lane (chunk a.chunk from a.start); else the
 // tail numbers 64 (b - mb) + lane (chunk 1 from a.tail).
 __device__ __forceinline__ void pers_unit(const Fd2Args &a, u32 b, u32 mb, u32 lane, bool &active, u64 &lo,
-                                          u64 &hi, u32 &chunk, u64 &off, bool &tailp) {
+                                          u64 &hi, u32 &chunk) {
     if (b < mb) {
         const u32 unit = 64 * b + lane;
         active = unit < a.nunits;
         lo = a.start_lo;
         hi = a.start_hi;
-        off = (u64)unit * a.chunk;
-        tailp = false;
+        add_u128(lo, hi, (u64)unit * a.chunk);
         chunk = a.chunk;
     } else {
         const u32 idx = 64 * (b - mb) + lane;
         active = idx < a.tail_count;
         lo = a.tail_lo;
         hi = a.tail_hi;
-        off = idx;
-        tailp = true;
+        add_u128(lo, hi, (u64)idx);
         chunk = 1;
     }
-    add_u128(lo, hi, off);
 }
 
 template <class P>
@@ -1819,14 +1817,14 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
     __shared__ u32 pers_next;
     u32 pmb = 0, pnk = 0, pk = 0;
     u64 n0_off = 0;          // n0 - the part's first n (init_at)
-    bool n0_tail = !main_part;
+    const bool n0_tail = !main_part;
     if constexpr (P::PERS) {
         pmb = (a.nunits + 63) / 64;
         const u32 nb = pmb + (a.tail_count + 63) / 64, G = gridDim.x;
         pnk = nb > blockIdx.x ? (nb - blockIdx.x + G - 1) / G : 0;
         pk = tid >> 6;
         if (tid == 0) pers_next = P::WG / 64;
-        if (pk < pnk) pers_unit(a, blockIdx.x + G * pk, pmb, lane_id, active, n0_lo, n0_hi, chunk_l, n0_off, n0_tail);
+        if (pk < pnk) pers_unit(a, blockIdx.x + G * pk, pmb, lane_id, active, n0_lo, n0_hi, chunk_l);
         else active = false;
     } else {
         n0_off = (u64)unit * chunk;
@@ -1865,7 +1863,13 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
         }
     }
     State<P> st;
-    if (!sib_done && active) init_at<P>(st, n0_tail ? a.xt : a.xs, n0_off, n0_lo, n0_hi);
+    // (the persistent grid runs only on the 1024-thread kernels, which keep
+    // init(): C64)
+    if constexpr (P::PERS || P::N64 || P::C64) {
+        if (!sib_done && active) init<P>(st, n0_lo, n0_hi);
+    } else {
+        if (!sib_done && active) init_at<P>(st, n0_tail ? a.xt : a.xs, n0_off, n0_lo, n0_hi);
+    }
     // The table DMA must have landed before any wave reads LDS: wait for it
     // explicitly (a workgroup barrier alone need not imply vmcnt(0)), then
     // the barrier.
@@ -1894,10 +1898,8 @@ __device__ __forceinline__ void fd2_body(const Fd2Args &a) {
         u32 ch = chunk_l;
         while (k < pnk) {
             if (taken) {
-                u64 off = 0;
-                bool tp = false;
-                pers_unit(a, blockIdx.x + gridDim.x * k, pmb, lane_id, act, m_lo, m_hi, ch, off, tp);
-                if (act) init_at<P>(st, tp ? a.xt : a.xs, off, m_lo, m_hi);
+                pers_unit(a, blockIdx.x + gridDim.x * k, pmb, lane_id, act, m_lo, m_hi, ch);
+                if (act) init<P>(st, m_lo, m_hi);
             }
             if (act) walk_chunk<P>(st, smem, ch, m_lo, m_hi, hbase, hinc, outl, cutoff, out, probe_acc);
             if (++taken >= a.wave_cap) break;
