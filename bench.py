@@ -40,20 +40,30 @@ import os
 import sys
 import time
 
-# Hardware queues per process: at N = 1 HIP's default (4, what the GPU box
-# exports and what a Rust client linking libnice_hip.so gets).  Under torchrun
-# the process also holds torch's stream and RCCL's next to the library's six
-# slot streams, and on 4 queues the exchange's copies and collective wait
-# behind queued field kernels: a 1/8 shard's step is 0.281 ms at 4 queues,
-# 0.264 at 8, 0.263 at 16 (plain process: 0.259; profiles/r03/dist_hw_queues.log),
-# so the distributed driver asks for 8.  --hw-queues N overrides (A/B runs).
-# Set before HIP initialises; the value used and the exported one are recorded
-# in the JSON line's config.
+# Hardware queues per process: HIP's default (4, what the GPU box exports and
+# what a Rust client linking libnice_hip.so gets), also under torchrun when
+# the field exchange runs in shared memory (the default on one node: no device
+# work besides the library's six slot streams).  With the exchange over RCCL
+# the process also holds torch's stream and RCCL's, and on 4 queues the
+# exchange's copies and collective wait behind queued field kernels: a 1/8
+# shard's step is 0.281 ms at 4 queues, 0.264 at 8, 0.263 at 16 (plain
+# process: 0.259; profiles/r03/dist_hw_queues.log), so that path asks for 8.
+# --hw-queues N overrides (A/B runs).  Set before HIP initialises; the value
+# used and the exported one are recorded in the JSON line's config.
 HW_QUEUES_EXPORTED = os.environ.get("GPU_MAX_HW_QUEUES")
+
+
+def _argv(flag, default):
+    return sys.argv[sys.argv.index(flag) + 1] if flag in sys.argv[:-1] else default
+
+
 if "--hw-queues" in sys.argv:
-    os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[sys.argv.index("--hw-queues") + 1]
+    os.environ["GPU_MAX_HW_QUEUES"] = _argv("--hw-queues", "4")
 elif "WORLD_SIZE" in os.environ:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+    _ex = _argv("--exchange-backend", "auto")
+    _one_node = os.environ.get("LOCAL_WORLD_SIZE", os.environ["WORLD_SIZE"]) == os.environ["WORLD_SIZE"]
+    if _ex == "nccl" or (_ex == "auto" and not _one_node and _argv("--dist-backend", "nccl") == "nccl"):
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -85,6 +95,12 @@ def parse():
                    help="niceonly MSD filter placement (same candidate set either way)")
     p.add_argument("--depth", type=int, default=2, choices=[1, 2],
                    help="fields kept in flight behind the one being collected")
+    p.add_argument("--exchange-lag", type=int, default=2, choices=[1, 2, 3],
+                   help="N > 1: field exchanges kept in flight (PipelinedExchange lag)")
+    p.add_argument("--exchange-backend", choices=["auto", "shm", "nccl", "gloo"], default="auto",
+                   help="N > 1: the per-field exchange in node-local shared memory (shm), over "
+                        "the process group's RCCL on device buffers (nccl), or over a gloo group "
+                        "on host tensors (gloo); auto = shm when every rank is on this node")
     p.add_argument("--probe-lib", action="store_true",
                    help="A/B experiments: load the probe build (env tuning knobs live only there)")
     p.add_argument("--two-ctx", action="store_true",
@@ -304,9 +320,30 @@ def main(args):
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
+    # The per-field exchange: its vector (~1 KiB) is host
+    # data at both ends, so on one node the ranks sum it in shared memory; over
+    # RCCL every step queues an H2D copy, the collective and a D2H copy behind
+    # the field kernels for CU slots.
+    ex_group, ex_kind = None, None
+    if dist is not None:
+        ex_kind = args.exchange_backend
+        if ex_kind == "auto":
+            ex_kind = "shm" if int(os.environ.get("LOCAL_WORLD_SIZE", world)) == world else args.dist_backend
+        if ex_kind == "gloo" and args.dist_backend != "gloo":
+            ex_group = dist.new_group(backend="gloo")
+        if ex_kind == "nccl" and args.dist_backend != "nccl":
+            raise SystemExit("bench.py: --exchange-backend nccl needs --dist-backend nccl")
 
     import nice_amd as N
     from nice_amd import dist as D
+    shm_ex = None
+    if ex_kind == "shm":
+        try:
+            shm_ex = D.ShmExchange(dist, lag=args.exchange_lag)
+        except D.ShmUnavailable as e:  # raised on every rank alike
+            print(f"bench.py: shared-memory exchange unavailable ({e}); exchanging over "
+                  f"{args.dist_backend}", file=sys.stderr)
+            ex_kind = args.dist_backend + " (shm unavailable)"
 
     br = N.get_base_range_u128(base)
     strong = args.scaling == "strong" or world == 1
@@ -349,11 +386,13 @@ def main(args):
     def make_pipeline(d):
         # detailed-only / niceonly-only runs pass a context that skips the other mode
         return D.FieldPipeline(det_ctx if modes[0] else _Skip(), nice_ctx if modes[1] else _Skip(),
-                               d, depth=args.depth, **nice_opts)
+                               d, group=ex_group if d is not None else None,
+                               exchange=shm_ex if d is not None else None,
+                               depth=args.depth, lag=args.exchange_lag, **nice_opts)
 
     if args.sync:
         runner = N.BothModes(local, det_ctx=det_ctx, nice_ctx=nice_ctx)
-        ex = D.PipelinedExchange(dist) if dist is not None else None
+        ex = shm_ex or (D.PipelinedExchange(dist, ex_group) if dist is not None else None)
         kern = []
 
         def step():
@@ -413,7 +452,8 @@ def main(args):
     if args.mode == "both" and not args.sync:
         for name, sel in (("detailed", (True, False)), ("niceonly", (False, True))):
             p1 = D.FieldPipeline(det_ctx if sel[0] else _Skip(), nice_ctx if sel[1] else _Skip(),
-                                 dist, depth=args.depth, **nice_opts)
+                                 dist, group=ex_group, exchange=shm_ex, depth=args.depth,
+                                 lag=args.exchange_lag, **nice_opts)
 
             def step1(p1=p1):
                 r = p1.step(field, base)
@@ -468,6 +508,8 @@ def main(args):
     if rank != 0:
         if args.sync:
             runner.close()
+        if shm_ex is not None:
+            shm_ex.close()
         dist.destroy_process_group()
         return
 
@@ -505,6 +547,8 @@ def main(args):
             "dist_backend": args.dist_backend if dist is not None else None,
             "pipelined": not args.sync,
             "pipeline_depth": None if args.sync else args.depth,
+            "exchange_lag": args.exchange_lag if dist is not None else None,
+            "exchange_backend": ex_kind,
             "probe_lib": PROBE_LIB,
             "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
             "gpu_max_hw_queues_exported": HW_QUEUES_EXPORTED,
@@ -589,6 +633,8 @@ def main(args):
     print(json.dumps(line), file=json_out, flush=True)
     if args.sync:
         runner.close()
+    if shm_ex is not None:
+        shm_ex.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -28,12 +28,18 @@ shard is empty (a field smaller than the world) contributes zeros to the
 collective instead of calling the library.
 
 With the nccl backend the collectives are RCCL over xGMI on device tensors;
-with gloo (the CPU tests) they run on host tensors.  `shard_fn` lets tests
+with gloo (the CPU tests) they run on host tensors.  The per-field SUM of a
+pipelined run has two transports: PipelinedExchange (the group's collective)
+and ShmExchange (node-local shared memory, no device work; bench.py's default
+when every rank is on one node).  `shard_fn` lets tests
 substitute a shard processor; the default is the HIP library.
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
 
 from .types import FieldResults, FieldSize, NiceNumberSimple, UniquesDistributionSimple
 
@@ -204,18 +210,24 @@ class PipelinedExchange:
     """Overlap each field's exchange with the next field's compute: submit()
     starts the all-reduce of this field's [histogram, counts] vector
     asynchronously (RCCL runs it while the ranks process the next field) and
-    returns the PREVIOUS field's reduced vector; drain() returns the last one.
+    returns the reduced vector of the field submitted `lag` calls earlier (the
+    previous one by default); drain() / drain_all() return the rest.
     The lists of a field are gathered when its vector is collected (only if
-    non-empty, which is rare).  Two preallocated device vectors alternate, fed
+    non-empty, which is rare).  lag+1 preallocated device vectors rotate, fed
     from / read back into pinned host memory; on a GPU the read-back is queued
     behind the collective at submit time and marked by an event, so a step
     costs three asynchronous enqueues and collecting the previous field only
     waits on an event that has long fired (no synchronous copy on the
     launching thread)."""
 
-    def __init__(self, dist, group=None, width: int = 0):
+    def __init__(self, dist, group=None, width: int = 0, lag: int = 1):
+        # lag: submissions between a field's submit() and the one that returns
+        # its vector (1 = the next one); lag+1 buffer sets rotate
+        if lag < 1:
+            raise ValueError("PipelinedExchange: lag must be >= 1")
         self.dist, self.group = dist, group
-        self.pending = None
+        self.lag = lag
+        self.pending = []
         self.width = 0
         self.bufs = []
         self.flip = 0
@@ -228,8 +240,8 @@ class PipelinedExchange:
         pin = dev.type == "cuda"
         self.bufs = [(torch.zeros(width, dtype=torch.int64, pin_memory=pin),
                       torch.zeros(width, dtype=torch.int64, device=dev),
-                      torch.zeros(width, dtype=torch.int64, pin_memory=pin)) for _ in range(2)]
-        self.events = [torch.cuda.Event() for _ in range(2)] if pin else None
+                      torch.zeros(width, dtype=torch.int64, pin_memory=pin)) for _ in range(self.lag + 1)]
+        self.events = [torch.cuda.Event() for _ in range(self.lag + 1)] if pin else None
         self.width = width
 
     def submit(self, vals: Sequence[int], payload):
@@ -238,7 +250,7 @@ class PipelinedExchange:
             self._alloc(len(vals))
         h_in, d, h_out = self.bufs[self.flip]
         ev = self.events[self.flip] if self.events is not None else None
-        self.flip ^= 1
+        self.flip = (self.flip + 1) % (self.lag + 1)
         h_in.numpy()[:] = vals
         d.copy_(h_in, non_blocking=True)
         work = self.dist.all_reduce(d, op=self.dist.ReduceOp.SUM, group=self.group, async_op=True)
@@ -249,16 +261,22 @@ class PipelinedExchange:
             h_out.copy_(d, non_blocking=True)
             ev.record()
             work = ev
-        prev, self.pending = self.pending, (work, d, h_out, payload)
-        return self._collect(prev)
+        self.pending.append((work, d, h_out, payload))
+        return self._collect(self.pending.pop(0)) if len(self.pending) > self.lag else None
 
     def drain_check(self):
-        if self.pending is not None:
+        if self.pending:
             raise RuntimeError("PipelinedExchange: drain() before changing the vector width")
 
     def drain(self):
-        prev, self.pending = self.pending, None
-        return self._collect(prev)
+        """The oldest pending field's (vector, payload), or None."""
+        return self._collect(self.pending.pop(0)) if self.pending else None
+
+    def drain_all(self):
+        out = []
+        while self.pending:
+            out.append(self._collect(self.pending.pop(0)))
+        return out
 
     def _collect(self, p):
         if p is None:
@@ -270,6 +288,126 @@ class PipelinedExchange:
             work.wait()
             h_out.copy_(d)
         return h_out.tolist(), payload
+
+
+class ShmUnavailable(RuntimeError):
+    """Raised on EVERY rank when some rank cannot map the shared array."""
+
+
+class ShmExchange:
+    """PipelinedExchange's interface (submit / drain / drain_all) with the SUM
+    done in node-local shared memory: the field's exchange vector is host data
+    at both ends (the histogram comes back through the library's mapped
+    result words, the counts are list lengths), so when every rank of the
+    group runs on this host the ranks write their vectors into their rows of
+    one /dev/shm array and each sums the column block itself.  No device copy
+    and no collective kernel is queued behind the field kernels, and no
+    transport latency is paid; the rare near-miss / nice lists still go
+    through the group's collective (_gather_rows).
+
+    Layout: int64 [2*lag + 2 sets][world][1 + width]; a rank writes its row's
+    values, then the row's sequence word (= submission index + 1).  A set is
+    rewritten 2*lag + 2 submissions later, and a rank can only be that far
+    ahead of the slowest reader after that reader has published (its collect
+    of s - lag waits for every row of s - lag), so no row is overwritten
+    while it can still be read; collect checks the sequence words anyway.
+    x86 stores are seen in program order, so a row whose sequence word is
+    current holds that submission's values."""
+
+    def __init__(self, dist, group=None, width: int = 0, lag: int = 1, timeout_s: float = 300.0):
+        import platform
+        import secrets
+        if lag < 1:
+            raise ValueError("ShmExchange: lag must be >= 1")
+        if platform.machine() not in ("x86_64", "AMD64"):
+            raise RuntimeError("ShmExchange relies on x86 store ordering")
+        self.dist, self.group = dist, group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self.lag, self.sets = lag, 2 * lag + 2
+        self.width = width or MAX_BINS + 2 * self.world
+        self.timeout_s = timeout_s
+        name = [f"/dev/shm/nice_ex_{os.getpid()}_{secrets.token_hex(6)}" if self.rank == 0 else None]
+        dist.broadcast_object_list(name, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                   group=group)
+        self.path = name[0]
+        shape = (self.sets, self.world, 1 + self.width)
+        self.buf, err = None, None
+        if self.rank == 0:
+            try:
+                self.buf = np.memmap(self.path, dtype=np.int64, mode="w+", shape=shape)
+                self.buf[:] = 0
+                self.buf.flush()
+            except OSError as e:
+                err = f"rank 0: {e}"
+        dist.barrier(group=group)
+        if self.rank != 0:
+            try:
+                self.buf = np.memmap(self.path, dtype=np.int64, mode="r+", shape=shape)
+            except OSError as e:  # another host, or no /dev/shm
+                err = f"rank {self.rank}: {e}"
+        errs = [None] * self.world
+        dist.all_gather_object(errs, err, group=group)
+        if self.rank == 0 and self.buf is not None:
+            os.unlink(self.path)  # the mappings stay; nothing is left behind in /dev/shm
+        if any(errs):
+            self.buf = None
+            raise ShmUnavailable("; ".join(e for e in errs if e))
+        self.step = 0
+        self.pending = []
+
+    def submit(self, vals: Sequence[int], payload):
+        if len(vals) != self.width:
+            raise ValueError(f"ShmExchange: vector of {len(vals)} values, the exchange holds {self.width}")
+        row = self.buf[self.step % self.sets, self.rank]
+        row[1:] = vals  # non-negative counts below 2**63 (numpy raises on anything else)
+        row[0] = self.step + 1
+        self.pending.append((self.step, payload))
+        self.step += 1
+        return self._collect(self.pending.pop(0)) if len(self.pending) > self.lag else None
+
+    def drain(self):
+        return self._collect(self.pending.pop(0)) if self.pending else None
+
+    def drain_all(self):
+        out = []
+        while self.pending:
+            out.append(self._collect(self.pending.pop(0)))
+        return out
+
+    def drain_check(self):
+        if self.pending:
+            raise RuntimeError("ShmExchange: drain() first")
+
+    def _collect(self, p):
+        import time
+        step, payload = p
+        blk = self.buf[step % self.sets]
+        seq = blk[:, 0]
+        deadline = None
+        spins = 0
+        while True:
+            if (seq == step + 1).all():
+                break
+            if (seq > step + 1).any():
+                raise RuntimeError("ShmExchange: a row was overwritten before it was read")
+            spins += 1
+            if spins > 64:
+                now = time.monotonic()
+                deadline = deadline or now + self.timeout_s
+                if now > deadline:
+                    raise TimeoutError(f"ShmExchange: ranks {list(np.flatnonzero(seq != step + 1))} "
+                                       f"never published submission {step}")
+                time.sleep(20e-6)
+        red = blk[:, 1:].sum(axis=0).tolist()
+        if not (seq == step + 1).all():
+            raise RuntimeError("ShmExchange: a row was overwritten while it was read")
+        return red, payload
+
+    def close(self):
+        """Drop this rank's mapping (no collective: the other ranks' mappings
+        keep the memory until the last one is closed)."""
+        self.pending = []
+        self.buf = None
 
 
 def process_field_both_pipelined(ex: PipelinedExchange, range_: FieldSize, base: int, ctx,
@@ -348,7 +486,8 @@ class FieldPipeline:
     and is dealt every N-th niceonly chunk of it (see module doc); with
     dist=None the whole field runs on this process's contexts."""
 
-    def __init__(self, det_ctx, nice_ctx, dist=None, group=None, depth: int = 2, **nice_opts):
+    def __init__(self, det_ctx, nice_ctx, dist=None, group=None, depth: int = 2, lag: int = 1,
+                 exchange=None, **nice_opts):
         # depth: fields kept in flight behind the one being collected (the
         # library holds up to 3 per mode and context)
         self.depth = depth
@@ -356,7 +495,11 @@ class FieldPipeline:
         self.dist, self.group = dist, group
         self.rank = dist.get_rank(group) if dist is not None else 0
         self.world = dist.get_world_size(group) if dist is not None else 1
-        self.ex = PipelinedExchange(dist, group) if dist is not None else None
+        # exchange: a PipelinedExchange / ShmExchange to use (drained by every
+        # drain()), else a PipelinedExchange over `group` with `lag`
+        # exchanges kept in flight
+        self.ex = exchange if exchange is not None or dist is None else \
+            PipelinedExchange(dist, group, lag=lag)
         self.nice_opts = dict(nice_opts)
         self.inflight = []  # (range, base, det ticket or None, nice ticket or None)
         self.kernel_ms = []  # detailed kernel time of each collected field (HIP events)
@@ -406,9 +549,7 @@ class FieldPipeline:
             if r is not None:
                 out.append(r)
         if self.ex is not None:
-            r = self._finish(self.ex.drain())
-            if r is not None:
-                out.append(r)
+            out.extend(self._finish(c) for c in self.ex.drain_all())
         return out
 
 

@@ -2,6 +2,7 @@
 rehearsal of the N = 8 path): weak-scaling
 field assignment (disjoint consecutive 1e9 fields, all inside base 40's range)
 and the max-over-ranks timing reduction."""
+import contextlib
 import os
 import socket
 
@@ -184,6 +185,36 @@ def _field_worker(rank, world, port, q):
                                     [(d.num_uniques, d.count) for d in det.distribution],
                                     [(n.number, n.num_uniques) for n in det.nice_numbers],
                                     [n.number for n in nic.nice_numbers]) for r, det, nic, _ in got]
+    # two exchanges in flight (bench.py --exchange-lag 2): the same results, in order
+    pipe = D.FieldPipeline(_OracleCtx(), _OracleCtx(), dist, lag=2, chunk_size=997)
+    got = [pipe.step(f, b) for f, b in mixed]
+    assert got == [None] * 4  # depth 2 + lag 2: a field's results come back 4 steps later
+    got = [g for g in got if g is not None] + pipe.drain()
+    res["field_pipeline_lag2"] = [((r.range_start, r.range_end), len(det.distribution),
+                                   [(d.num_uniques, d.count) for d in det.distribution],
+                                   [(n.number, n.num_uniques) for n in det.nice_numbers],
+                                   [n.number for n in nic.nice_numbers]) for r, det, nic, _ in got]
+    # the node-local shared-memory exchange (bench.py --exchange-backend shm), lag 1 and 2
+    for lag in (1, 2):
+        ex = D.ShmExchange(dist, lag=lag)
+        pipe = D.FieldPipeline(_OracleCtx(), _OracleCtx(), dist, exchange=ex, chunk_size=997)
+        got = [pipe.step(f, b) for f, b in mixed]
+        got = [g for g in got if g is not None] + pipe.drain()
+        ex.close()
+        res[f"field_pipeline_shm{lag}"] = [((r.range_start, r.range_end), len(det.distribution),
+                                           [(d.num_uniques, d.count) for d in det.distribution],
+                                           [(n.number, n.num_uniques) for n in det.nice_numbers],
+                                           [n.number for n in nic.nice_numbers]) for r, det, nic, _ in got]
+    # one rank unable to map the array: every rank raises ShmUnavailable (no hang)
+    import unittest.mock
+    import numpy
+    with unittest.mock.patch.object(numpy, "memmap", side_effect=OSError("no /dev/shm")) \
+            if rank == 1 else contextlib.nullcontext():
+        try:
+            D.ShmExchange(dist)
+            res["shm_unavailable"] = None
+        except D.ShmUnavailable as e:
+            res["shm_unavailable"] = str(e)
     q.put((rank, res))
     dist.destroy_process_group()
 
@@ -233,6 +264,9 @@ def test_two_rank_field_sharding_matches_single_process():
         w = O.process_range_detailed(a, b, base)
         assert (d, near) == (w.distribution, w.nice_numbers), base
         assert nice == _oracle_niceonly_shard(a, b, base, 997), base
+    assert out[0]["field_pipeline_lag2"] == mixed
+    assert out[0]["field_pipeline_shm1"] == mixed and out[0]["field_pipeline_shm2"] == mixed
+    assert out[0]["shm_unavailable"] == "rank 1: no /dev/shm"
     w = O.process_range_detailed(69, 70, 10)
     assert out[0]["tiny"] == (w.distribution, [(69, 10)])
     assert out[0]["tiny_both"] == (w.distribution, [(69, 10)], [69])
@@ -268,6 +302,16 @@ def _eight_worker(rank, world, port, q):
                               [(d.num_uniques, d.count) for d in det.distribution],
                               [(n.number, n.num_uniques) for n in det.nice_numbers],
                               [n.number for n in nic.nice_numbers]) for r, det, nic, _ in got]
+    # the same over the shared-memory exchange (bench.py's default at N > 1 on one node)
+    ex = D.ShmExchange(dist, lag=2)
+    pipe = D.FieldPipeline(_OracleCtx(), _OracleCtx(), dist, exchange=ex, chunk_size=97)
+    got = [pipe.step(f, b) for f, b in fields]
+    got = [g for g in got if g is not None] + pipe.drain()
+    ex.close()
+    res["field_pipeline_shm"] = [((r.range_start, r.range_end),
+                                  [(d.num_uniques, d.count) for d in det.distribution],
+                                  [(n.number, n.num_uniques) for n in det.nice_numbers],
+                                  [n.number for n in nic.nice_numbers]) for r, det, nic, _ in got]
     q.put((rank, res))
     dist.destroy_process_group()
 
@@ -299,6 +343,7 @@ def test_eight_rank_rehearsal():
         w = O.process_range_detailed(a, b, base)
         assert (d, near) == (w.distribution, w.nice_numbers), (a, base)
         assert nice == _oracle_niceonly_shard(a, b, base, 97), (a, base)
+    assert out[0]["field_pipeline_shm"] == out[0]["field_pipeline"]
 
 
 def test_both_modes_runner_matches_sequential_and_propagates_errors():
