@@ -2310,15 +2310,32 @@ static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s
     // 0.263-0.289 against 0.282-0.307; 9e7 ties; profiles/r05/
     // sib_small_L.log; the 4- and 8-way shards of the bench field,
     // shard_projection.log).
+    // A field that overlaps a running one (pipelined submits) shares the chip
+    // with it, so no round is part-filled and the per-number cost decides:
+    // the large-field pick.  The 8-way shard of the bench field (1.25e8),
+    // pipelined: 0.2412 ms per step at L = 105, 0.2422 at 81, 0.2481 at the
+    // small-field pick (79 / 81 / 65 by shard); 2.5e8 0.486 / 0.494 / 0.500,
+    // 5e7 0.110 / 0.113 / 0.112, 1e8 0.1940 / 0.1938 / 0.1952, and L = 125
+    // 20-25 % slower everywhere (profiles/r06/exchange/small_L_pipe.log).
     const u64 Q0 = p.count / SB;
-    if (!L && 10 * Q0 * (D / P::TCHUNK) < 60 * lanes) {
+    if (!L && !p.overlapped && 10 * Q0 * (D / P::TCHUNK) < 60 * lanes) {
         double rounds = 0;
         L = pick_small_stride<P>(seg_start, p.count, P::TCHUNK * 3 / 4, P::TCHUNK * 5 / 4, P::LO + 1, Q0, lanes, D,
                                  rounds);
         if (10 * rounds < (double)probe_knob("NICE_FD2_SIBROUNDS", 15))
             return launch_cfg<typename P::NoSib>(p, num_cus, s);
     }
-    if (!L) L = pick_lane_stride<P>(seg_start, p.count, P::TCHUNK * 3 / 4, P::TCHUNK * 3 / 2, P::TCHUNK, P::LO + 1);
+    // Target stride: TCHUNK, or 140 for the pipelined walk (LG >= 100), which
+    // fills and drains its lookup pipeline once per unit and so gains from
+    // longer units.  b40 bench field (pipelined, stride swept over odd L in
+    // [61, 255] against the pick, profiles/r06/stride/): target 80 picked
+    // 65 at 1e9 (1.917 ms per field), target 140 picks 143 (-2.5 %) there and
+    // 159 at 1.25e8 (-2.7 %); a quarter into the range -0.6 / -2.8 %.  The
+    // per-sibling-lookup kernels (LG 1, b40 beyond the first limb layout and
+    // b42..55) gain nothing consistent from longer targets (b42 1.25e8 +14 %
+    // at 140), so they keep TCHUNK.
+    constexpr u64 T = P::LG >= 100 ? 140 : (u64)P::TCHUNK;
+    if (!L) L = pick_lane_stride<P>(seg_start, p.count, T * 3 / 4, T * 3 / 2, T, P::LO + 1);
     // chunks reach low-digit entries n mod B + i < LDE (Cfg::LDE)
     constexpr u64 LMAX = (u64)P::LDE - P::B;
     if (L % 2 == 0) L++;

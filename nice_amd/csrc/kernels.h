@@ -49,6 +49,9 @@ struct DetailedLaunch {
     uint32_t *launches;          // if set, incremented per kernel launch enqueued
     uint32_t *sib;               // fd2, if set: [0] sibling lanes M of the field's last sibling-lane
                                  // launch (0: none ran), [1] its lane stride L
+    uint32_t overlapped;         // fd2: another field of the device was still running when this one
+                                 // was enqueued (the pipelined case), so launches are shaped for
+                                 // throughput, not for the latency of a lone field
 };
 
 // Production FD kernel (fd2_detailed.hip): bases 40, 50, 80, in-range segments.

@@ -145,6 +145,7 @@ struct Slot {
     uint32_t *d_msd_mapped = nullptr, *d_nice_mapped = nullptr;  // device views
     uint32_t *d_nice_done = nullptr;  // workgroups retired (niceonly in-kernel finish)
     bool dirty = true;            // state block not known to be zero
+    bool inflight = false;        // a detailed field enqueued and not yet gathered
     bool timed = false;           // the detailed field records ev0 / ev1 (kernel timing)
     bool marked = false;          // ... or an untimed end marker (ev_done) on a shared stream
     uint64_t seq = 0;             // last detailed field's sequence number
@@ -522,6 +523,15 @@ int enqueue_detailed(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, bool *f
     p.out = nice::NumOut{sl.det.n, sl.det.u, sl.d_count, sl.det.cap};
     p.launches = &sl.launches;
     p.sib = sl.sib;
+    // Another detailed field of this device submitted and not yet collected:
+    // the caller pipelines, so this field's launches are shaped for throughput
+    // (launch_sib).  Whether that field is still running does not matter --
+    // fields on the slot streams progress together and often finish
+    // together, and a pick that followed their completion flipped every third
+    // 2.5e8 field to the lone-field stride (8 % slower per step,
+    // profiles/r06/stride/probe_pick.log).
+    for (const Slot &o : d.slot)
+        if (&o != &sl && o.inflight) p.overlapped = 1;
     *finished = false;
     // Small fields run wholly by fd2 publish tagged result words
     // (FieldFinish::tag): one fewer round trip to host memory at their end.
@@ -701,6 +711,7 @@ int enqueue_detailed_shard(Device &d, Slot &sl, u128 s, u128 e, uint32_t base, b
     bool finished = false;
     int rc = enqueue_detailed(d, sl, s, e, base, &finished);
     if (rc) return rc;
+    sl.inflight = true;
     if (timing) HIPCHK(hipEventRecord(sl.ev1, sl.stream));
     sl.fin_seq = finished;
     if (!finished) {
@@ -761,6 +772,7 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
         int rc = wait_field(sl);
         if (rc) return rc;
         sl.dirty = false;  // the epilogue zeroed the state block
+        sl.inflight = false;
         d.stats_slot = t;  // kernel_ms read on demand (resolve_stats)
         d.last.numbers = (uint64_t)(job.bounds[i + 1] - job.bounds[i]);
         d.last.launches = sl.launches;
@@ -777,6 +789,7 @@ int detailed_gather(nice_ctx *ctx, DetJob &job, int t) {
             if (!rc) rc = wait_field(sl);
             if (rc) return rc;
             sl.dirty = false;
+            sl.inflight = false;
             d.stats_slot = t;
             d.last.launches = sl.launches;
             d.last.sib_lanes = sl.sib[0];
@@ -881,7 +894,7 @@ int detailed_collect(nice_ctx *ctx, int t, uint64_t *hist, nice_number *out, siz
         int rc = detailed_gather(ctx, job, t);
         if (rc) {
             job.active = false;  // the field is lost; its slot is reusable
-            for (auto &d : ctx->devs) d.slot[t].dirty = true;
+            for (auto &d : ctx->devs) d.slot[t].dirty = true, d.slot[t].inflight = false;
             return rc;
         }
         job.collected = true;
@@ -1074,7 +1087,7 @@ int detailed_collect_locked(nice_ctx *ctx, int ticket, uint64_t *hist, nice_numb
         job.waiting = false;
         if (rc) {
             job.active = false;
-            for (auto &d : ctx->devs) d.slot[ticket].dirty = true;
+            for (auto &d : ctx->devs) d.slot[ticket].dirty = true, d.slot[ticket].inflight = false;
             return rc;
         }
     }
