@@ -1365,17 +1365,19 @@ def _stride_field(base, frac):
 
 
 @pytest.mark.parametrize("base,frac,strides", [
-    (40, 0.0, range(45, 121, 2)),                 # the bench layout: pipelined walk, VALU-decoded C2
-    (40, 0.5, (45, 61, 79, 81, 97, 119)),         # the per-sibling lookup-group walk
-    (52, 0.2, range(45, 121, 2)),                 # two lanes over the short low-digit table
+    (40, 0.0, range(45, 211, 2)),                 # the bench layout: pipelined walk, VALU-decoded C2
+    (40, 0.5, (45, 61, 79, 81, 97, 119, 143, 181, 209)),  # the per-sibling lookup-group walk
+    (52, 0.2, range(45, 241, 2)),                 # two lanes over the short low-digit table
 ])
 def test_every_sibling_lane_stride(ctx, base, frac, strides):
     """the sibling kernels pick their lane stride L per
-    launch (pick_lane_stride over odd L in [0.75, 1.5] TCHUNK, pick_small_stride
+    launch (pick_lane_stride over odd L in [0.75, 1.5] T -- T = 140 for the
+    pipelined walk, else TCHUNK: 80 at b40, 160 at b52 -- pick_small_stride
     over [0.75, 1.25] TCHUNK, fd2_kernel.hpp), and every L that does not divide
     B^2 leaves an edge unit per super-block.  With the stride forced through
-    nice_debug_force_sib_stride, each odd L in [45, 120] (b40, M = 3, and b52,
-    M = 2) runs a field of 4 super-blocks plus a ragged remainder -- whole
+    nice_debug_force_sib_stride, each odd L of those ranges ([45, 210] on the
+    b40 bench layout, M = 3; [45, 240] on b52, M = 2; a sample on b40's other
+    walk) runs a field of 4 super-blocks plus a ragged remainder -- whole
     super-blocks, one edge unit each, the regular remainder part -- and must
     equal the oracle's histogram and near-miss list bit for bit; the kernel
     stats must show the sibling kernel ran at that L."""
