@@ -274,9 +274,10 @@ struct Cfg {
     // static_assert below), normalised by 32-bit multiply-highs
     // VD & 65536 (probe A/B): the round-5 init -- init_digits on the 128-bit n
     // and u64 columns -- also on the 512-thread kernels of the bases whose n
-    // passes 64 bits
+    // passes 64 bits; the persistent-grid probe configurations at 512
+    // threads (PERS_ = 1) take it too, their init being the round-5 one
     static constexpr bool OLDINIT = (VD_ & 65536) != 0;
-    static constexpr bool C64 = !N64 && (WG_ >= 1024 || OLDINIT);
+    static constexpr bool C64 = !N64 && (WG_ >= 1024 || OLDINIT || PERS_ > 0);
     static constexpr int NS = cdiv(D2, 2), NC = cdiv(D3, 2), NX = cdiv(DN, 2);
     static constexpr int SL = ND + 1, CL = NE + 1, EL = NE2 + 1;  // per-step limbs
     static constexpr int S_TOPD = D2 - 2 * (NS - 1), C_TOPD = D3 - 2 * (NC - 1);

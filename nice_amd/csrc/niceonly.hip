@@ -930,7 +930,7 @@ template <class G>
 static hipError_t launch_nice(const NiceonlyLaunch &p, const G &g, int num_cus, hipStream_t s) {
     u64 waves = p.n_leaves_dev ? (u64)num_cus * 32 : ((u64)p.n_leaves + 7) / 8;
     u64 grid = (waves + 3) / 4;
-    const u64 cap = (u64)num_cus * 8;
+    const u64 cap = probe_knob("NICE_NICE_GRID", (u64)num_cus * 8);
     if (grid > cap) grid = cap;
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL(niceonly_kernel<G>, dim3((u32)grid), dim3(256), 0, s, p, g);
