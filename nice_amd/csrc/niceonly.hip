@@ -930,6 +930,8 @@ template <class G>
 static hipError_t launch_nice(const NiceonlyLaunch &p, const G &g, int num_cus, hipStream_t s) {
     u64 waves = p.n_leaves_dev ? (u64)num_cus * 32 : ((u64)p.n_leaves + 7) / 8;
     u64 grid = (waves + 3) / 4;
+    // (probe NICE_NICE_GRID: caps of 128..2048 workgroups tie on the bench
+    // step, 1.25e8 and 1e9; profiles/r06/niceonly/nice_grid.log)
     const u64 cap = probe_knob("NICE_NICE_GRID", (u64)num_cus * 8);
     if (grid > cap) grid = cap;
     if (grid < 1) grid = 1;
@@ -990,6 +992,11 @@ static hipError_t launch_msd(const MsdLaunch &p, const G &g, int num_cus, hipStr
     return hipGetLastError();
 }
 
+// (Measured and not kept, round 6: one wave per chunk instead of four.  On
+// the bench field's first 1.25e8 numbers, which have no survivors, the
+// pipelined step was 1.3 % faster; on the whole 1e9 field 0.7 % slower (the
+// niceonly chain 0.061 against 0.040 ms) and on the 8-way dealt shares, the
+// N = 8 load, 0.7-0.9 % slower; profiles/r06/niceonly/msd_wg.log, sp_wg.log.)
 template <class G, u32 MC = 0>
 static hipError_t launch_fused(const MsdLaunch &p, const G &g, ChunkNode *scratch, u32 cap, u32 grid,
                                hipStream_t s) {
