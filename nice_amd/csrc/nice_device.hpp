@@ -216,7 +216,9 @@ static inline GenericBase make_generic(u32 base) {
 constexpr uint32_t kDoneGroups = 64, kDoneWords = kDoneGroups + 1;
 __device__ __forceinline__ bool last_block_arrive(uint32_t *done) {
     const uint32_t g = blockIdx.x % kDoneGroups, n = gridDim.x;
-    // small grids: one counter (saves an L2 round trip on the critical path)
+    // small grids: one counter (saves an L2 round trip on the critical path;
+    // one counter for every grid up to 4096 workgroups made b40 1e6 15.8 us
+    // against 14.8, the 391 arrivals contending: small_arrive_one_level.log)
     if (n <= kDoneGroups) return atomicAdd(&done[0], 1u) == n - 1;
     const uint32_t expect = g < n ? (n - 1 - g) / kDoneGroups + 1 : 0;
     if (atomicAdd(&done[1 + g], 1u) != expect - 1) return false;
