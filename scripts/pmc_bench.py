@@ -55,14 +55,17 @@ ap.add_argument("--xcds", type=int, default=8)
 ap.add_argument("--valu-cpi", type=float, default=None,
                 help="issue cycles per VALU instruction of the hot loop (ISA budget)")
 ap.add_argument("--valu-cpi-source", default=None, help="file the --valu-cpi figure comes from")
-ap.add_argument("dirs", nargs="+")
+ap.add_argument("dirs", nargs="+", help="pass directories (rocprofv3 -d) or counter_collection CSV files")
 a = ap.parse_args()
 
 vals = collections.defaultdict(list)
 names = set()
 files = []
 for d in a.dirs:
-    for path in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
+    # a pass's output directory, or a committed copy of its counter CSV
+    paths = [d] if os.path.isfile(d) else sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"),
+                                                             recursive=True))
+    for path in paths:
         files.append(path)
         per = collections.defaultdict(float)
         for r in csv.DictReader(open(path)):
