@@ -1,3 +1,4 @@
+# (Record of a round-6 A/B: the NICE_FD2_CHAIN probe was removed after it)
 # Chained pipelined fields (probe NICE_FD2_CHAIN, per mille of a field's fd2
 # part launched before the event the next field waits on; 0 = the product's
 # concurrent fields): GPU tests through the probe library with chaining on,
