@@ -424,6 +424,55 @@ def test_field_pipeline_single_process():
             [n for n, _ in O.process_field_niceonly_mt(f.range_start, f.range_end, 10, 2)[0].nice_numbers]
 
 
+class _OneRank:
+    """The slice of torch.distributed ShmExchange uses, for a 1-rank group."""
+
+    def get_rank(self, group=None):
+        return 0
+
+    def get_world_size(self, group=None):
+        return 1
+
+    def broadcast_object_list(self, objs, src=0, group=None):
+        pass
+
+    def barrier(self, group=None):
+        pass
+
+    def all_gather_object(self, out, obj, group=None):
+        out[0] = obj
+
+
+def test_shm_exchange_order_lag_and_guards():
+    """ShmExchange on one rank: each submit returns the vector submitted `lag`
+    calls earlier (summed over the ranks: itself here), drain_all returns the
+    rest in order, the /dev/shm file is gone once mapped, and a wrong width,
+    a lag below 1 and a row overwritten before it was read all raise."""
+    from nice_amd import dist as D
+    d = _OneRank()
+    with pytest.raises(ValueError):
+        D.ShmExchange(d, lag=0)
+    for lag in (1, 2, 3):
+        ex = D.ShmExchange(d, lag=lag)
+        assert not os.path.exists(ex.path)
+        w = ex.width
+        vecs = [[k * 1000 + i for i in range(w)] for k in range(7)]
+        got = [ex.submit(v, k) for k, v in enumerate(vecs)]
+        assert got[:lag] == [None] * lag
+        got = [g for g in got[lag:]] + ex.drain_all()
+        assert [k for _, k in got] == list(range(7))
+        assert all(red == vecs[k] for red, k in got)
+        with pytest.raises(ValueError):
+            ex.submit([0] * (w - 1), None)
+        # a row rewritten past its set's reuse distance is detected, not read
+        ex.submit(vecs[0], "a")
+        step = ex.step - 1
+        ex.buf[step % ex.sets, 0, 0] = step + 1 + ex.sets
+        with pytest.raises(RuntimeError):
+            ex.drain()
+        ex.close()
+
+
 def test_bench_refuses_a_world_size_other_than_gpus():
     """bench.py under a launcher whose WORLD_SIZE differs from --gpus exits
     non-zero before touching a device (a run that would time another number
