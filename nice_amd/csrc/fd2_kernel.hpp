@@ -2336,6 +2336,16 @@ static hipError_t launch_sib(const DetailedLaunch &p, int num_cus, hipStream_t s
     // b42..55) gain nothing consistent from longer targets (b42 1.25e8 +14 %
     // at 140), so they keep TCHUNK.
     constexpr u64 T = P::LG >= 100 ? 140 : (u64)P::TCHUNK;
+    // A lone field of the pipelined walk (a synchronous caller, the reference
+    // client's pattern: nothing overlaps its last round) picks over the same
+    // range by whole rounds, as the small-field path does: b40 1e9 alone
+    // 1875-1887 us at L = 159 (7.99 rounds) against 1890-1947 at the model's
+    // 143 (8.9 rounds), 5e8 953 against 973-1012 (profiles/r06/stride/
+    // iso_L.log).  Pipelined fields keep the model's pick (no last round).
+    if (!L && P::LG >= 100 && !p.overlapped) {
+        double rounds = 0;
+        L = pick_small_stride<P>(seg_start, p.count, T * 3 / 4, T * 3 / 2, P::LO + 1, Q0, lanes, D, rounds);
+    }
     if (!L) L = pick_lane_stride<P>(seg_start, p.count, T * 3 / 4, T * 3 / 2, T, P::LO + 1);
     // chunks reach low-digit entries n mod B + i < LDE (Cfg::LDE)
     constexpr u64 LMAX = (u64)P::LDE - P::B;

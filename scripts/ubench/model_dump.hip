@@ -27,6 +27,14 @@ static int dump(u128 start, u64 count, int lo, int hi) {
     for (u64 t : {80ull, 100ull, 140ull, 160ull, 240ull})
         printf("pick_lane_stride target %llu: %llu\n", (unsigned long long)t,
                (unsigned long long)pick_lane_stride<P>(start, count, t * 3 / 4, t * 3 / 2, t, P::LO + 1));
+    // the lone-field rounds pick (launch_sib, LG >= 100) at 2 x 512-thread
+    // workgroups per CU on 256 CUs
+    if constexpr (P::SIB > 1) {
+        constexpr u64 D = (u64)P::B * P::B, SB = (u64)P::SIB * D;
+        double rounds = 0;
+        const u64 L = pick_small_stride<P>(start, count, 105, 210, P::LO + 1, count / SB, 262144, D, rounds);
+        printf("rounds pick [105, 210]: %llu (%.3f rounds)\n", (unsigned long long)L, rounds);
+    }
     return 0;
 }
 
