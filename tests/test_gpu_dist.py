@@ -87,19 +87,21 @@ def test_two_rank_strong_pipeline_on_gpu():
     assert res[0]["massive"][2] == [] and res[1]["massive"][2] == []
 
 
-@pytest.mark.parametrize("launcher", ["torchrun", "self"])
-def test_bench_two_ranks_strong_scaling_branch(launcher):
+@pytest.mark.parametrize("launcher,exchange", [("torchrun", "auto"), ("self", "auto"), ("torchrun", "gloo")])
+def test_bench_two_ranks_strong_scaling_branch(launcher, exchange):
     """bench.py's N > 1 path end to end, with gloo collectives so two ranks can
     share the one GPU of the test box -- as the driver's scaling run launches
     it (torch.distributed.run, one process per rank), and as a bare
     `bench.py --gpus 2`, which starts that launcher itself as a child process:
     the line carries n_gpus 2 and the strong-scaling fields (t1_ms_per_step,
     strong_efficiency, parallelism strong2) and every field of the timed
-    region came back whole and was checked (fields_checked == steps)."""
+    region came back whole and was checked (fields_checked == steps).  The
+    per-field sum runs in shared memory (auto: both ranks on this node) and,
+    in the last case, over the process group's collective."""
     import subprocess
     import sys
     args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
-            "--no-cpu-baseline", "--dist-backend", "gloo"]
+            "--no-cpu-baseline", "--dist-backend", "gloo", "--exchange-backend", exchange]
     if launcher == "torchrun":
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
@@ -114,6 +116,8 @@ def test_bench_two_ranks_strong_scaling_branch(launcher):
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "strong2"
     assert line["config"]["dist_backend"] == "gloo"
+    assert line["config"]["exchange_backend"] == ("shm" if exchange == "auto" else exchange)
+    assert line["config"]["exchange_lag"] == 2
     assert line["fields_checked"] == 6
     assert line["t1_ms_per_step"] > 0 and 0 < line["strong_efficiency"] < 2
     assert line["value"] > 0 and line["roofline"]["numbers_per_launch"] == 5 * 10 ** 8
